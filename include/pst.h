@@ -1,0 +1,143 @@
+/*
+ * pst.h — C ABI of libpst, the MI355X-native structure-tokenization path
+ * (PDB atom37 arrays → residue k-NN graph → MPNN encoder → cross-attention downsampler →
+ * FSQ token ids). Plain pointers and sizes; no torch types.
+ *
+ * What each entry point replaces in the reference (xwang112358/protein-structure-tokenizer):
+ *   pst_create       InferenceRunner.prepare_tokenize_fn + load_params/device_put_replicated
+ *                    (scripts/inference_runner.py:180-191, 237-248): one context per GPU holding
+ *                    the encoder-half parameters and precomputed input-independent tables.
+ *   pst_tokenize     make_graph_from_pdb → preprocess_sample (structure_tokenizer/data/
+ *                    preprocessing.py:42-283; graph build: utils/protein_utils.py:636-749,
+ *                    model/quat_affine.py:406-522) + the pmap'd Vq3D.encode_and_quantize
+ *                    (model/model.py:453-479) + tokens D2H (scripts/inference_runner.py:303-306).
+ *                    Host buffers in, host token ids out (synchronous).
+ *   pst_tokenize_device  the same on device-resident buffers, asynchronous on the context's
+ *                    stream (what a pipelined runner or bench uses: inputs already in HBM).
+ *   pst_aux_device   the non-token QuantizerOutput fields (quantize, continuous_embedding,
+ *                    continuous_embedding_pre_proj; model/quantize.py:183-242).
+ *   pst_sync / pst_last_error / pst_destroy   runtime plumbing (block_until_ready, errors).
+ *
+ * Errors: every call returns PST_OK (0) or a negative PST_E* code; pst_last_error(ctx) gives
+ * the message. The Python layer maps PST_E_TOO_LARGE / PST_E_TOO_SMALL to NotImplementedError
+ * and PST_E_INVALID to ValueError, the reference's exception types.
+ *
+ * Threading: one context per GPU; contexts are independent and may be driven from different
+ * host threads; a single context is not thread-safe.
+ */
+#ifndef PST_H_
+#define PST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PST_ABI_VERSION 1
+
+enum {
+  PST_OK = 0,
+  PST_E_INVALID = -1,    /* bad argument / shape (ValueError) */
+  PST_E_TOO_LARGE = -2,  /* protein > seq_max_size residues (NotImplementedError) */
+  PST_E_TOO_SMALL = -3,  /* protein < graph_max_neighbor residues (NotImplementedError) */
+  PST_E_HIP = -4,        /* HIP runtime error */
+  PST_E_NOMEM = -5,
+};
+
+/* Model hyper-parameters (config/structure_tokenizer/model/gnn/ablation_*_df_*.yaml). */
+typedef struct {
+  int32_t abi_version;        /* = PST_ABI_VERSION */
+  int32_t codebook_size;      /* 432 | 1728 | 4096 | 64000 (= prod(levels)) */
+  int32_t downsampling_ratio; /* df: 1 | 2 | 4 */
+  int32_t n_levels;           /* D = codes_dimension (5 or 6) */
+  int32_t levels[8];          /* FSQ levels, e.g. {4,4,4,4,4,4} or {8,8,8,5,5,5} */
+  int32_t seq_max_size;       /* 512: proteins above it are rejected */
+  int32_t graph_max_neighbor; /* k = 50 */
+} pst_model_desc;
+
+/*
+ * Parameter blob: float32, the encoder-half tensors of Vq3D in haiku shapes, row-major,
+ * concatenated in this order (names after params_keys_conversion; "ENC" =
+ * vq3_d/~/structure_encoder, "L" = ENC/~/graph_neural_network/~/mpnn_layer{,_1,_2},
+ * "DS" = vq3_d/~/cross_attn_downsampling/cross_attn_scaler_iteration):
+ *   ENC/init_node_embed w[128,128] b[128];  ENC/init_edge_embed w[155,128] b[128]
+ *   3 x { L/node_mlp_0/~/linear_{0,1,2} w[384|128|128,128] b[128];
+ *         L/node_mlp_1/~/linear_0 w[128,512] b[512]; L/node_mlp_1/~/linear_1 w[512,128] b[128];
+ *         L/edge_mlp/~/linear_{0,1,2} (as node_mlp_0);
+ *         L/norm_msg{,_1,_2} scale[128] offset[128] }
+ *   DS/cross_attention/{query_norm,data_norm} scale[3,128] offset[3,128]
+ *   DS/cross_attention/attention query_w key_w value_w gating_w [3,128,4,32]
+ *                                gating_b[3,4,32] output_w[3,4,32,128] output_b[3,128]
+ *   DS/{resampled,original}_transition: input_layer_norm scale[3,128] offset[3,128],
+ *        transition1 weights[3,128,256] bias[3,256], transition2 weights[3,256,128] bias[3,128]
+ *   vq3_d/down_proj w[128,D] b[D]
+ * (pst_amd/params.py:param_spec is the same list.)
+ */
+size_t pst_param_count(int32_t n_levels);
+
+typedef struct pst_ctx pst_ctx;
+
+int pst_create(int32_t device, const pst_model_desc* desc, const float* params, size_t n_params,
+               pst_ctx** out);
+int pst_destroy(pst_ctx* ctx);
+const char* pst_last_error(const pst_ctx* ctx);
+/* Last error of a failed pst_create (no context exists yet). */
+const char* pst_create_error(void);
+
+/*
+ * Tokenize a ragged batch of B proteins (host buffers, synchronous).
+ *   atom_pos     [R,37,3] float64   atom37 coordinates (R = prot_offsets[B])
+ *   atom_flags   [R,37]   uint8     bit0 = atom37_gt_exists, bit1 = atom37_atom_exists
+ *   prot_offsets [B+1]    int64     residue offsets of each protein in the arrays above
+ *   tokens_out   [R]      uint32    protein b's ids at tokens_out[prot_offsets[b] ...]
+ *   n_tokens_out [B]      int32     floor(n_b / df), n_b = residues with N, CA, C and O
+ *   n_nodes_out  [B]      int32     n_b (may be NULL)
+ * Each protein must have graph_max_neighbor <= R_b <= seq_max_size residues
+ * (scripts/inference_runner.py:52-62), else PST_E_TOO_SMALL / PST_E_TOO_LARGE.
+ */
+int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags,
+                 const int64_t* prot_offsets, int32_t n_prot, uint32_t* tokens_out,
+                 int32_t* n_tokens_out, int32_t* n_nodes_out);
+
+/*
+ * Same on device buffers (d_* in HBM of ctx's device), asynchronous on ctx's stream.
+ * prot_offsets stays a HOST array (it sizes the launch). Outputs are device buffers with the
+ * layout of pst_tokenize. Call pst_sync before reading them.
+ */
+int pst_tokenize_device(pst_ctx* ctx, const double* d_atom_pos, const uint8_t* d_atom_flags,
+                        const int64_t* prot_offsets, int32_t n_prot, uint32_t* d_tokens_out,
+                        int32_t* d_n_tokens_out, int32_t* d_n_nodes_out);
+
+/*
+ * Non-token QuantizerOutput fields of the LAST tokenize call, copied to host:
+ *   bounded  [R, D]   continuous_embedding (tanh-bounded latents, masked)
+ *   quantize [R, D]   quantize (rounded codes)
+ *   pre_proj [R, 128] continuous_embedding_pre_proj (spherical-normalised)
+ * Rows are laid out like tokens_out. Any pointer may be NULL.
+ */
+int pst_aux(pst_ctx* ctx, float* bounded, float* quantize, float* pre_proj);
+
+/*
+ * FSQ aux over the implicit codebook for the LAST call (model/quantize.py:226-239):
+ *   distances [T, K]  sum_d (b_d - c_kd)^2, soft_proba [T, K] softmax(distances) (either may be
+ *   NULL), argmin [T] uint32 (nearest code; equals the token id except at exact .5 ties).
+ * T = number of token rows of the last call (sum of n_tokens_out), host buffers.
+ */
+int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t* argmin);
+
+int pst_sync(pst_ctx* ctx);
+
+/* Stream the context launches on (hipStream_t), for event timing by callers. */
+void* pst_stream(pst_ctx* ctx);
+
+/* Debug: copy an intermediate of the LAST call to host.
+ *   which = 0..3: node features after init embed / MPNN layer 1..3, [R,128] (raw slot rows)
+ *   which = 10:   edge features [R*k, 32] float (27 used), which = 11: senders [R*k] int32 */
+int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PST_H_ */

@@ -1,0 +1,28 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "protein-structure-tokenizer_amd")
+for p in (ROOT, PKG, os.path.join(ROOT, "tests", "golden")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
+    config.addinivalue_line("markers", "reference: runs the reference's own code under the test shim "
+                                       "(needs /root/reference; skipped elsewhere)")
+
+
+def pytest_collection_modifyitems(config, items):
+    import _refenv
+    if not _refenv.available():
+        skip = pytest.mark.skip(reason="/root/reference not present")
+        for it in items:
+            if "reference" in it.keywords:
+                it.add_marker(skip)
+
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")

@@ -1,0 +1,34 @@
+"""`jax.nn` subset in NumPy (test shim); formulas as published by JAX 0.4.23."""
+import numpy as _np
+
+
+def gelu(x, approximate=True):
+    if approximate:
+        c = _np.sqrt(2 / _np.pi).astype(x.dtype)
+        cdf = 0.5 * (1.0 + _np.tanh(c * (x + 0.044715 * (x ** 3))))
+        return x * cdf
+    from scipy.special import erf
+    return x * (1 + erf(x / _np.sqrt(2))) / 2
+
+
+def relu(x):
+    return _np.maximum(x, 0)
+
+
+def sigmoid(x):
+    return 1.0 / (1.0 + _np.exp(-x))
+
+
+def swish(x):
+    return x * sigmoid(x)
+
+
+def softmax(x, axis=-1):
+    m = _np.max(x, axis=axis, keepdims=True)
+    u = _np.exp(x - m)
+    return u / _np.sum(u, axis=axis, keepdims=True)
+
+
+def one_hot(x, num_classes, dtype=_np.float64):
+    x = _np.asarray(x)
+    return (x[..., None] == _np.arange(num_classes)).astype(dtype)
