@@ -1,0 +1,744 @@
+// pst_api.cpp — C ABI of libpst (include/pst.h): contexts, weight re-layout, workspace,
+// launch sequence. Host code only; kernels live in pst_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pst.h"
+#include "pst_kernels.h"
+
+namespace {
+
+constexpr int H = 128;
+constexpr int KNN = 50;
+
+thread_local std::string g_create_error;
+
+int tile_channel(int h, int M, int r) { return 32 * M + (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// ------------------------------------------------------------------ parameter views
+struct Lin {
+  const float* w;
+  const float* b;
+};
+struct Layer {
+  Lin msg[3], ff[2], edge[3];
+  const float *ln_s[3], *ln_o[3];
+};
+struct HostParams {
+  Lin node_embed, edge_embed;
+  Layer L[3];
+  const float *qn_s, *qn_o, *dn_s, *dn_o, *qw, *kw, *vw, *gw, *gb, *ow, *ob;
+  const float *rt_ln_s, *rt_ln_o, *rt_w1, *rt_b1, *rt_w2, *rt_b2;
+  const float *ot_ln_s, *ot_ln_o, *ot_w1, *ot_b1, *ot_w2, *ot_b2;
+  Lin down;
+};
+
+size_t walk(const float* base, int D, HostParams* P) {
+  size_t o = 0;
+  auto take = [&](size_t n) {
+    const float* r = base ? base + o : nullptr;
+    o += n;
+    return r;
+  };
+  P->node_embed = {take(H * H), take(H)};
+  P->edge_embed = {take((H + 27) * H), take(H)};
+  for (int l = 0; l < 3; ++l) {
+    Layer& m = P->L[l];
+    m.msg[0] = {take(3 * H * H), take(H)};
+    m.msg[1] = {take(H * H), take(H)};
+    m.msg[2] = {take(H * H), take(H)};
+    m.ff[0] = {take(H * 4 * H), take(4 * H)};
+    m.ff[1] = {take(4 * H * H), take(H)};
+    m.edge[0] = {take(3 * H * H), take(H)};
+    m.edge[1] = {take(H * H), take(H)};
+    m.edge[2] = {take(H * H), take(H)};
+    for (int i = 0; i < 3; ++i) {
+      m.ln_s[i] = take(H);
+      m.ln_o[i] = take(H);
+    }
+  }
+  P->qn_s = take(3 * H); P->qn_o = take(3 * H);
+  P->dn_s = take(3 * H); P->dn_o = take(3 * H);
+  P->qw = take(3 * H * H); P->kw = take(3 * H * H); P->vw = take(3 * H * H);
+  P->gw = take(3 * H * H); P->gb = take(3 * H);
+  P->ow = take(3 * H * H); P->ob = take(3 * H);
+  P->rt_ln_s = take(3 * H); P->rt_ln_o = take(3 * H);
+  P->rt_w1 = take(3 * H * 2 * H); P->rt_b1 = take(3 * 2 * H);
+  P->rt_w2 = take(3 * 2 * H * H); P->rt_b2 = take(3 * H);
+  P->ot_ln_s = take(3 * H); P->ot_ln_o = take(3 * H);
+  P->ot_w1 = take(3 * H * 2 * H); P->ot_b1 = take(3 * 2 * H);
+  P->ot_w2 = take(3 * 2 * H * H); P->ot_b2 = take(3 * H);
+  P->down = {take((size_t)H * D), take(D)};
+  return o;
+}
+
+// ------------------------------------------------------------------ device re-layout
+// Everything device-side lives in one arena; builders append and return element offsets.
+struct Arena {
+  std::vector<float> h;
+  size_t add(const std::vector<float>& v) {
+    size_t o = h.size();
+    h.insert(h.end(), v.begin(), v.end());
+    while (h.size() % 64) h.push_back(0.0f);  // 256-B alignment for every array
+    return o;
+  }
+};
+
+// A fragments of a GEMM over K input channels [k0, k0+Kc) (Kc = 128 -> 64 k-steps, 32 -> 16)
+// and outputs [o0, o0+128): frag[t][lane][M] = W[k0 + c(t,h)][o0 + 32 M + (lane&31)].
+std::vector<float> frag(const float* W, int ldw, int k0, int Kvalid, int Kc, int o0, int Ovalid) {
+  int steps = Kc / 2;
+  std::vector<float> f((size_t)steps * 64 * 4, 0.0f);
+  for (int t = 0; t < steps; ++t)
+    for (int lane = 0; lane < 64; ++lane) {
+      int c = tile_channel(lane >> 5, t / 16, t % 16);
+      for (int M = 0; M < 4; ++M) {
+        int o = 32 * M + (lane & 31);
+        float v = 0.0f;
+        if (c < Kvalid && o < Ovalid) v = W[(size_t)(k0 + c) * ldw + o0 + o];
+        f[((size_t)t * 64 + lane) * 4 + M] = v;
+      }
+    }
+  return f;
+}
+
+std::vector<float> frag_narrow(const float* W, int ldw, int O) {  // K = 128, outputs < O
+  std::vector<float> f(64 * 64, 0.0f);
+  for (int t = 0; t < 64; ++t)
+    for (int lane = 0; lane < 64; ++lane) {
+      int c = tile_channel(lane >> 5, t / 16, t % 16);
+      int o = lane & 31;
+      if (o < O) f[t * 64 + lane] = W[(size_t)c * ldw + o];
+    }
+  return f;
+}
+
+std::vector<float> perm(const float* v) {  // 128-vector → perm order
+  std::vector<float> p(128);
+  for (int h = 0; h < 2; ++h)
+    for (int M = 0; M < 4; ++M)
+      for (int r = 0; r < 16; ++r) p[h * 64 + M * 16 + r] = v[tile_channel(h, M, r)];
+  return p;
+}
+
+std::vector<float> perm_rows(const std::vector<float>& nat, int rows) {
+  std::vector<float> out((size_t)rows * 128);
+  for (int i = 0; i < rows; ++i) {
+    auto p = perm(nat.data() + (size_t)i * 128);
+    std::copy(p.begin(), p.end(), out.begin() + (size_t)i * 128);
+  }
+  return out;
+}
+
+std::vector<float> cat(std::initializer_list<std::vector<float>> parts) {
+  std::vector<float> out;
+  for (auto& p : parts) out.insert(out.end(), p.begin(), p.end());
+  return out;
+}
+
+// positional_encoding_layer.py:49-66 with a float32 argument
+float pe_value(int x, int n, int k1) {
+  int num = (k1 & 1) ? 2 * (k1 - 1) : 2 * k1;
+  float e = (float)num / 128.0f;
+  float pw = (float)std::pow((double)n, (double)e);
+  float arg = ((float)x * 3.14159274101257324f) / pw;
+  return (float)((k1 & 1) ? std::cos((double)arg) : std::sin((double)arg));
+}
+
+std::vector<float> pe_rows(int x0, int count, int n) {
+  std::vector<float> out((size_t)count * 128);
+  for (int i = 0; i < count; ++i)
+    for (int k = 1; k <= 128; ++k) out[(size_t)i * 128 + k - 1] = pe_value(x0 + i, n, k);
+  return out;
+}
+
+struct MlpOff {
+  size_t w0, b0, w1, b1, w2, b2;
+};
+struct LayerOff {
+  MlpOff msg, edge;
+  size_t ff_w1, ff_b1, ff_w2, ff_b2, proj;  // proj: filled per kernel
+  size_t ln_s[3], ln_o[3];
+};
+struct BlockOff {
+  size_t qn_s, qn_o, dn_s, dn_o, wq, wk, wv, wg, wo, gb, ob;
+  size_t rt_ln_s, rt_ln_o, rt_w1, rt_b1, rt_w2, rt_b2;
+  size_t ot_ln_s, ot_ln_o, ot_w1, ot_b1, ot_w2, ot_b2;
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------ context
+struct pst_ctx {
+  int device = 0;
+  pst_model_desc desc{};
+  int D = 6, df = 1, max_out = 512;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // weights arena (device) + offsets
+  float* d_arena = nullptr;
+  size_t emb_w = 0, emb_b = 0;
+  LayerOff L[3]{};
+  size_t proj[2]{};
+  BlockOff B[3]{};
+  size_t down_w = 0, down_b = 0;
+  // tables (device, separate allocations)
+  float *d_h0 = nullptr, *d_PM0 = nullptr, *d_T = nullptr, *d_RPE = nullptr;
+  float fsq_half[8]{}, fsq_off[8]{}, fsq_shift[8]{};
+  int fsq_L[8]{}, fsq_basis[8]{};
+  // workspace (grow-only)
+  int64_t cap_R = 0;
+  int cap_B = 0;
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  // per-call layout
+  int64_t last_R = 0, last_Rpad = 0;
+  int last_B = 0;
+  struct {
+    int64_t* offsets;
+    int32_t *n_nodes, *node_local, *node_prot, *senders, *deg, *tile_prot, *tile_t0;
+    double *frame, *cen, *ca;
+    float *feat, *e0, *e1, *h0, *h1, *P0, *P1, *r_buf, *v_buf, *bounded, *quant, *pre_proj;
+    double* pos;
+    uint8_t* flags;
+    uint32_t* tokens;
+    int32_t* n_tok;
+  } w{};
+  std::vector<int64_t> h_offsets;
+  float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
+  int64_t dbg_cap = 0;
+};
+
+namespace {
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) {                                                         \
+      ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);                    \
+      return PST_E_HIP;                                                             \
+    }                                                                               \
+  } while (0)
+
+int fail(pst_ctx* ctx, int code, const std::string& msg) {
+  ctx->err = msg;
+  return code;
+}
+
+int build_weights(pst_ctx* ctx, const float* blob) {
+  HostParams P;
+  walk(blob, ctx->D, &P);
+  Arena A;
+  ctx->emb_w = A.add(frag(P.edge_embed.w, H, 128, 27, 32, 0, 128));
+  ctx->emb_b = A.add(perm(P.edge_embed.b));
+  for (int l = 0; l < 3; ++l) {
+    const Layer& S = P.L[l];
+    LayerOff& O = ctx->L[l];
+    auto mlp = [&](const Lin* m, MlpOff& o) {
+      o.w0 = A.add(frag(m[0].w, H, 256, 128, 128, 0, 128));
+      o.b0 = A.add(perm(m[0].b));
+      o.w1 = A.add(frag(m[1].w, H, 0, 128, 128, 0, 128));
+      o.b1 = A.add(perm(m[1].b));
+      o.w2 = A.add(frag(m[2].w, H, 0, 128, 128, 0, 128));
+      o.b2 = A.add(perm(m[2].b));
+    };
+    mlp(S.msg, O.msg);
+    mlp(S.edge, O.edge);
+    std::vector<float> w1, b1, w2;
+    for (int ck = 0; ck < 4; ++ck) {
+      auto f = frag(S.ff[0].w, 4 * H, 0, 128, 128, 128 * ck, 128);
+      w1.insert(w1.end(), f.begin(), f.end());
+      auto bp = perm(S.ff[0].b + 128 * ck);
+      b1.insert(b1.end(), bp.begin(), bp.end());
+      auto g = frag(S.ff[1].w, H, 128 * ck, 128, 128, 0, 128);
+      w2.insert(w2.end(), g.begin(), g.end());
+    }
+    O.ff_w1 = A.add(w1);
+    O.ff_b1 = A.add(b1);
+    O.ff_w2 = A.add(w2);
+    O.ff_b2 = A.add(perm(S.ff[1].b));
+    for (int i = 0; i < 3; ++i) {
+      O.ln_s[i] = A.add(perm(S.ln_s[i]));
+      O.ln_o[i] = A.add(perm(S.ln_o[i]));
+    }
+  }
+  // projections produced by kernel l for kernel l+1: [E_s, E_r] (edge MLP of layer l),
+  // [M_s, M_r] (message MLP of layer l+1): first-layer rows 0..127 / 128..255, no bias
+  for (int l = 0; l < 2; ++l) {
+    const Layer& S = P.L[l];
+    const Layer& N = P.L[l + 1];
+    ctx->proj[l] = A.add(cat({frag(S.edge[0].w, H, 0, 128, 128, 0, 128), frag(S.edge[0].w, H, 128, 128, 128, 0, 128),
+                              frag(N.msg[0].w, H, 0, 128, 128, 0, 128), frag(N.msg[0].w, H, 128, 128, 128, 0, 128)}));
+  }
+  for (int b = 0; b < 3; ++b) {
+    BlockOff& O = ctx->B[b];
+    const size_t v = (size_t)b * H, m = (size_t)b * H * H;
+    O.qn_s = A.add(perm(P.qn_s + v)); O.qn_o = A.add(perm(P.qn_o + v));
+    O.dn_s = A.add(perm(P.dn_s + v)); O.dn_o = A.add(perm(P.dn_o + v));
+    O.wq = A.add(frag(P.qw + m, H, 0, 128, 128, 0, 128));
+    O.wk = A.add(frag(P.kw + m, H, 0, 128, 128, 0, 128));
+    O.wv = A.add(frag(P.vw + m, H, 0, 128, 128, 0, 128));
+    O.wg = A.add(frag(P.gw + m, H, 0, 128, 128, 0, 128));
+    O.gb = A.add(perm(P.gb + v));
+    O.wo = A.add(frag(P.ow + m, H, 0, 128, 128, 0, 128));
+    O.ob = A.add(perm(P.ob + v));
+    auto trans = [&](const float* ln_s, const float* ln_o, const float* w1, const float* b1, const float* w2,
+                     const float* b2, size_t& s, size_t& o, size_t& W1, size_t& B1, size_t& W2, size_t& B2) {
+      s = A.add(perm(ln_s + v));
+      o = A.add(perm(ln_o + v));
+      const float* w1b = w1 + (size_t)b * H * 2 * H;
+      const float* w2b = w2 + (size_t)b * 2 * H * H;
+      W1 = A.add(cat({frag(w1b, 2 * H, 0, 128, 128, 0, 128), frag(w1b, 2 * H, 0, 128, 128, 128, 128)}));
+      B1 = A.add(cat({perm(b1 + (size_t)b * 2 * H), perm(b1 + (size_t)b * 2 * H + 128)}));
+      W2 = A.add(cat({frag(w2b, H, 0, 128, 128, 0, 128), frag(w2b, H, 128, 128, 128, 0, 128)}));
+      B2 = A.add(perm(b2 + v));
+    };
+    trans(P.rt_ln_s, P.rt_ln_o, P.rt_w1, P.rt_b1, P.rt_w2, P.rt_b2, O.rt_ln_s, O.rt_ln_o, O.rt_w1, O.rt_b1, O.rt_w2,
+          O.rt_b2);
+    trans(P.ot_ln_s, P.ot_ln_o, P.ot_w1, P.ot_b1, P.ot_w2, P.ot_b2, O.ot_ln_s, O.ot_ln_o, O.ot_w1, O.ot_b1, O.ot_w2,
+          O.ot_b2);
+  }
+  ctx->down_w = A.add(frag_narrow(P.down.w, ctx->D, ctx->D));
+  std::vector<float> db(64, 0.0f);
+  for (int d = 0; d < ctx->D; ++d) db[d] = P.down.b[d];
+  ctx->down_b = A.add(db);
+  // staging inputs for the table GEMMs
+  auto nodePE = perm_rows(pe_rows(0, 512, 512), 512);
+  auto edgePE = perm_rows(pe_rows(-511, 1023, 512), 1023);
+  auto rpe = perm_rows(pe_rows(0, ctx->max_out, ctx->max_out), ctx->max_out);
+  size_t o_npe = A.add(nodePE), o_epe = A.add(edgePE);
+  size_t o_ne_w = A.add(frag(P.node_embed.w, H, 0, 128, 128, 0, 128)), o_ne_b = A.add(perm(P.node_embed.b));
+  size_t o_ee_w = A.add(frag(P.edge_embed.w, H, 0, 128, 128, 0, 128));
+  size_t o_m0s = A.add(frag(P.L[0].msg[0].w, H, 0, 128, 128, 0, 128));
+  size_t o_m0r = A.add(frag(P.L[0].msg[0].w, H, 128, 128, 128, 0, 128));
+
+  HIPCHK(hipMalloc(&ctx->d_arena, A.h.size() * sizeof(float)));
+  HIPCHK(hipMemcpy(ctx->d_arena, A.h.data(), A.h.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&ctx->d_h0, 512 * 128 * sizeof(float)));
+  HIPCHK(hipMalloc(&ctx->d_PM0, 512 * 256 * sizeof(float)));
+  HIPCHK(hipMalloc(&ctx->d_T, 1023 * 128 * sizeof(float)));
+  HIPCHK(hipMalloc(&ctx->d_RPE, (size_t)ctx->max_out * 128 * sizeof(float)));
+  HIPCHK(hipMemcpy(ctx->d_RPE, rpe.data(), rpe.size() * sizeof(float), hipMemcpyHostToDevice));
+  float* a = ctx->d_arena;
+  auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(a + o); };
+  pst::launch_table_gemm(a + o_npe, 512, F4(o_ne_w), a + o_ne_b, ctx->d_h0, 128, ctx->stream);
+  pst::launch_table_gemm(ctx->d_h0, 512, F4(o_m0s), nullptr, ctx->d_PM0, 256, ctx->stream);
+  pst::launch_table_gemm(ctx->d_h0, 512, F4(o_m0r), nullptr, ctx->d_PM0 + 128, 256, ctx->stream);
+  pst::launch_table_gemm(a + o_epe, 1023, F4(o_ee_w), nullptr, ctx->d_T, 128, ctx->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  // FSQ constants (quantize.py:175-181, computed in float32 as JAX does)
+  uint32_t basis = 1;
+  for (int d = 0; d < ctx->D; ++d) {
+    int L = ctx->desc.levels[d];
+    float half_l = ((float)(L - 1) * 0.999f) / 2.0f;
+    float off = (L % 2 == 0) ? 0.5f : 0.0f;
+    ctx->fsq_half[d] = half_l;
+    ctx->fsq_off[d] = off;
+    ctx->fsq_shift[d] = (float)std::tan((double)(off / half_l));
+    ctx->fsq_L[d] = L;
+    ctx->fsq_basis[d] = (int)basis;
+    basis *= (uint32_t)L;
+  }
+  return PST_OK;
+}
+
+int ensure_workspace(pst_ctx* ctx, int64_t R, int B) {
+  int64_t Rpad = (R + 127) / 128 * 128;
+  if (Rpad <= ctx->cap_R && B <= ctx->cap_B) return PST_OK;
+  Rpad = std::max<int64_t>(Rpad, ctx->cap_R);
+  B = std::max(B, ctx->cap_B);
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  ctx->ws = nullptr;
+  size_t E = (size_t)Rpad * KNN;
+  struct Item {
+    void** p;
+    size_t bytes;
+  };
+  auto& w = ctx->w;
+  std::vector<Item> items = {
+      {(void**)&w.offsets, sizeof(int64_t) * (B + 1)},   {(void**)&w.n_nodes, sizeof(int32_t) * B},
+      {(void**)&w.n_tok, sizeof(int32_t) * B},          {(void**)&w.tile_prot, sizeof(int32_t) * (Rpad / 32 + B)},
+      {(void**)&w.tile_t0, sizeof(int32_t) * (Rpad / 32 + B)},
+      {(void**)&w.node_local, sizeof(int32_t) * Rpad}, {(void**)&w.node_prot, sizeof(int32_t) * Rpad},
+      {(void**)&w.senders, sizeof(int32_t) * E},        {(void**)&w.deg, sizeof(int32_t) * Rpad},
+      {(void**)&w.frame, sizeof(double) * 9 * Rpad},    {(void**)&w.cen, sizeof(double) * 3 * Rpad},
+      {(void**)&w.ca, sizeof(double) * 3 * Rpad},       {(void**)&w.feat, sizeof(float) * 32 * E},
+      {(void**)&w.e0, sizeof(float) * 128 * E},         {(void**)&w.e1, sizeof(float) * 128 * E},
+      {(void**)&w.h0, sizeof(float) * 128 * Rpad},      {(void**)&w.h1, sizeof(float) * 128 * Rpad},
+      {(void**)&w.P0, sizeof(float) * 512 * Rpad},      {(void**)&w.P1, sizeof(float) * 512 * Rpad},
+      {(void**)&w.r_buf, sizeof(float) * 128 * Rpad},   {(void**)&w.v_buf, sizeof(float) * 128 * Rpad},
+      {(void**)&w.bounded, sizeof(float) * 8 * Rpad},   {(void**)&w.quant, sizeof(float) * 8 * Rpad},
+      {(void**)&w.pre_proj, sizeof(float) * 128 * Rpad}, {(void**)&w.pos, sizeof(double) * 37 * 3 * Rpad},
+      {(void**)&w.flags, sizeof(uint8_t) * 37 * Rpad},  {(void**)&w.tokens, sizeof(uint32_t) * Rpad},
+  };
+  size_t total = 0;
+  for (auto& it : items) total += (it.bytes + 4095) / 4096 * 4096;
+  hipError_t e = hipMalloc(&ctx->ws, total);
+  if (e != hipSuccess) {
+    ctx->ws = nullptr;
+    ctx->cap_R = 0;
+    ctx->cap_B = 0;
+    return fail(ctx, PST_E_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(e));
+  }
+  char* p = (char*)ctx->ws;
+  for (auto& it : items) {
+    *it.p = p;
+    p += (it.bytes + 4095) / 4096 * 4096;
+  }
+  ctx->ws_bytes = total;
+  const char* dbg = getenv("PST_DEBUG");
+  if (dbg && dbg[0] == '1') {
+    for (int l = 0; l < 3; ++l) {
+      if (ctx->dbg[l]) (void)hipFree(ctx->dbg[l]);
+      if (hipMalloc(&ctx->dbg[l], sizeof(float) * 128 * Rpad) != hipSuccess) ctx->dbg[l] = nullptr;
+    }
+  }
+  ctx->cap_R = Rpad;
+  ctx->cap_B = B;
+  return PST_OK;
+}
+
+int validate(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot) {
+  if (n_prot <= 0 || !offsets) return fail(ctx, PST_E_INVALID, "empty batch");
+  if (offsets[0] != 0) return fail(ctx, PST_E_INVALID, "prot_offsets[0] must be 0");
+  for (int b = 0; b < n_prot; ++b) {
+    int64_t r = offsets[b + 1] - offsets[b];
+    if (r > ctx->desc.seq_max_size)
+      return fail(ctx, PST_E_TOO_LARGE,
+                  "We currently don't support protein with more than " + std::to_string(ctx->desc.seq_max_size) +
+                      " residues given: " + std::to_string(r));
+    if (r < ctx->desc.graph_max_neighbor)
+      return fail(ctx, PST_E_TOO_SMALL,
+                  "We currently don't support protein with less than " +
+                      std::to_string(ctx->desc.graph_max_neighbor) + " residues given: " + std::to_string(r));
+  }
+  return PST_OK;
+}
+
+int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t* offsets, int32_t n_prot,
+        uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes) {
+  const int64_t R = offsets[n_prot];
+  int rc = ensure_workspace(ctx, R, n_prot);
+  if (rc) return rc;
+  auto& w = ctx->w;
+  const int64_t Rpad = (R + 127) / 128 * 128;
+  hipStream_t st = ctx->stream;
+  // per-protein token tiles of 32 (upper bound from the raw residue count)
+  std::vector<int32_t> tp, tt;
+  for (int b = 0; b < n_prot; ++b) {
+    int64_t Tmax = (offsets[b + 1] - offsets[b]) / ctx->df;
+    for (int64_t t0 = 0; t0 < Tmax; t0 += 32) {
+      tp.push_back(b);
+      tt.push_back((int32_t)t0);
+    }
+  }
+  ctx->h_offsets.assign(offsets, offsets + n_prot + 1);
+  HIPCHK(hipMemcpyAsync(w.offsets, ctx->h_offsets.data(), sizeof(int64_t) * (n_prot + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(w.tile_prot, tp.data(), sizeof(int32_t) * tp.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(w.tile_t0, tt.data(), sizeof(int32_t) * tt.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(w.node_local, 0xff, sizeof(int32_t) * Rpad, st));
+  HIPCHK(hipMemsetAsync(w.node_prot, 0, sizeof(int32_t) * Rpad, st));
+
+  pst::PrepArgs pa{d_pos, d_flags, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca};
+  pst::launch_prep(pa, n_prot, st);
+  pst::KnnArgs ka{Rpad, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, w.senders, w.deg, w.feat};
+  pst::launch_knn(ka, st);
+
+  const float* A = ctx->d_arena;
+  auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(A + o); };
+  auto mlp = [&](const MlpOff& o) {
+    return pst::MlpW{F4(o.w0), A + o.b0, F4(o.w1), A + o.b1, F4(o.w2), A + o.b2};
+  };
+  float* hbuf[4] = {nullptr, w.h0, w.h1, w.h0};
+  float* ebuf[3] = {w.e0, w.e1, nullptr};
+  float* pbuf[3] = {w.P0, w.P1, nullptr};
+  for (int l = 0; l < 3; ++l) {
+    pst::MpnnArgs m{};
+    m.n_tasks = Rpad / 32;
+    m.senders = w.senders;
+    m.deg = w.deg;
+    m.node_local = w.node_local;
+    m.feat = w.feat;
+    m.Ttab = ctx->d_T;
+    m.W_embed = F4(ctx->emb_w);
+    m.b_embed = A + ctx->emb_b;
+    m.PM0 = ctx->d_PM0;
+    m.h0tab = ctx->d_h0;
+    if (l > 0) {
+      m.e_in = ebuf[l - 1];
+      m.P_in = pbuf[l - 1];
+      m.h_in = hbuf[l];
+      m.edge = mlp(ctx->L[l - 1].edge);
+      m.edge_ln_s = A + ctx->L[l - 1].ln_s[2];
+      m.edge_ln_o = A + ctx->L[l - 1].ln_o[2];
+    }
+    const LayerOff& L = ctx->L[l];
+    m.msg = mlp(L.msg);
+    m.ln0_s = A + L.ln_s[0];
+    m.ln0_o = A + L.ln_o[0];
+    m.ln1_s = A + L.ln_s[1];
+    m.ln1_o = A + L.ln_o[1];
+    m.ff_w1 = F4(L.ff_w1);
+    m.ff_b1 = A + L.ff_b1;
+    m.ff_w2 = F4(L.ff_w2);
+    m.ff_b2 = A + L.ff_b2;
+    m.proj_w = l < 2 ? F4(ctx->proj[l]) : nullptr;
+    m.e_out = ebuf[l];
+    m.h_out = hbuf[l + 1];
+    m.P_out = pbuf[l];
+    pst::launch_mpnn(l, m, st);
+    if (ctx->dbg[l]) HIPCHK(hipMemcpyAsync(ctx->dbg[l], m.h_out, sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
+  }
+  // downsampler's original track works on a copy of h3 (h3 stays available to pst_debug_fetch)
+  HIPCHK(hipMemcpyAsync(w.h1, hbuf[3], sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
+  pst::DownArgs d{};
+  d.n_tiles = (int32_t)tp.size();
+  d.tile_prot = w.tile_prot;
+  d.tile_t0 = w.tile_t0;
+  d.offsets = w.offsets;
+  d.n_nodes = d_nnodes;
+  d.RPE = ctx->d_RPE;
+  d.o_buf = w.h1;
+  d.r_buf = w.r_buf;
+  d.v_buf = w.v_buf;
+  for (int b = 0; b < 3; ++b) {
+    const BlockOff& O = ctx->B[b];
+    pst::DownBlockW& W = d.blk[b];
+    W.qn_s = A + O.qn_s; W.qn_o = A + O.qn_o; W.dn_s = A + O.dn_s; W.dn_o = A + O.dn_o;
+    W.wq = F4(O.wq); W.wk = F4(O.wk); W.wv = F4(O.wv); W.wg = F4(O.wg); W.wo = F4(O.wo);
+    W.gb = A + O.gb; W.ob = A + O.ob;
+    W.rt_ln_s = A + O.rt_ln_s; W.rt_ln_o = A + O.rt_ln_o; W.rt_w1 = F4(O.rt_w1); W.rt_b1 = A + O.rt_b1;
+    W.rt_w2 = F4(O.rt_w2); W.rt_b2 = A + O.rt_b2;
+    W.ot_ln_s = A + O.ot_ln_s; W.ot_ln_o = A + O.ot_ln_o; W.ot_w1 = F4(O.ot_w1); W.ot_b1 = A + O.ot_b1;
+    W.ot_w2 = F4(O.ot_w2); W.ot_b2 = A + O.ot_b2;
+  }
+  d.down_w = A + ctx->down_w;
+  d.down_b = A + ctx->down_b;
+  d.D = ctx->D;
+  for (int i = 0; i < 8; ++i) {
+    d.fsq_half[i] = ctx->fsq_half[i];
+    d.fsq_off[i] = ctx->fsq_off[i];
+    d.fsq_shift[i] = ctx->fsq_shift[i];
+    d.fsq_L[i] = ctx->fsq_L[i] ? ctx->fsq_L[i] : 1;
+    d.fsq_basis[i] = ctx->fsq_basis[i];
+  }
+  d.tokens_out = d_tokens;
+  d.bounded_out = w.bounded;
+  d.quant_out = w.quant;
+  d.pre_proj_out = w.pre_proj;
+  if (d.n_tiles > 0) pst::launch_down(ctx->df, d, st);
+  HIPCHK(hipGetLastError());
+  ctx->last_R = R;
+  ctx->last_Rpad = Rpad;
+  ctx->last_B = n_prot;
+  (void)d_ntok;
+  return PST_OK;
+}
+
+__global__ void k_ntok(const int32_t* n_nodes, int32_t* n_tok, int B, int df) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) n_tok[b] = n_nodes[b] / df;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t pst_param_count(int32_t n_levels) {
+  HostParams P;
+  return walk(nullptr, n_levels, &P);
+}
+
+const char* pst_create_error(void) { return g_create_error.c_str(); }
+
+int pst_create(int32_t device, const pst_model_desc* desc, const float* params, size_t n_params, pst_ctx** out) {
+  g_create_error.clear();
+  if (!desc || !params || !out) {
+    g_create_error = "null argument";
+    return PST_E_INVALID;
+  }
+  if (desc->abi_version != PST_ABI_VERSION) {
+    g_create_error = "ABI version mismatch";
+    return PST_E_INVALID;
+  }
+  int D = desc->n_levels;
+  int df = desc->downsampling_ratio;
+  if (D < 1 || D > 8 || (df != 1 && df != 2 && df != 4) || desc->graph_max_neighbor != KNN ||
+      desc->seq_max_size != 512) {
+    g_create_error = "unsupported model description (need 1<=D<=8, df in {1,2,4}, k=50, seq_max_size=512)";
+    return PST_E_INVALID;
+  }
+  int64_t K = 1;
+  for (int d = 0; d < D; ++d) K *= desc->levels[d];
+  if (K != desc->codebook_size) {
+    g_create_error = "codebook_size != prod(levels)";
+    return PST_E_INVALID;
+  }
+  if (n_params != pst_param_count(D)) {
+    g_create_error = "parameter blob has " + std::to_string(n_params) + " floats, expected " +
+                     std::to_string(pst_param_count(D));
+    return PST_E_INVALID;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    g_create_error = "no such HIP device: " + std::to_string(device);
+    return PST_E_HIP;
+  }
+  pst_ctx* ctx = new pst_ctx();
+  ctx->device = device;
+  ctx->desc = *desc;
+  ctx->D = D;
+  ctx->df = df;
+  ctx->max_out = desc->seq_max_size / df;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    g_create_error = "hip stream creation failed";
+    delete ctx;
+    return PST_E_HIP;
+  }
+  int rc = build_weights(ctx, params);
+  if (rc) {
+    g_create_error = ctx->err;
+    pst_destroy(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return PST_OK;
+}
+
+int pst_destroy(pst_ctx* ctx) {
+  if (!ctx) return PST_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (int l = 0; l < 3; ++l)
+    if (ctx->dbg[l]) (void)hipFree(ctx->dbg[l]);
+  for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_RPE, ctx->ws})
+    if (p) (void)hipFree(p);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return PST_OK;
+}
+
+const char* pst_last_error(const pst_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void* pst_stream(pst_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int pst_sync(pst_ctx* ctx) {
+  if (!ctx) return PST_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return PST_OK;
+}
+
+int pst_tokenize_device(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t* offsets,
+                        int32_t n_prot, uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes) {
+  if (!ctx) return PST_E_INVALID;
+  ctx->err.clear();
+  int rc = validate(ctx, offsets, n_prot);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(ctx->device));
+  rc = run(ctx, d_pos, d_flags, offsets, n_prot, d_tokens, d_ntok, d_nnodes);
+  if (rc) return rc;
+  if (d_ntok) hipLaunchKernelGGL(k_ntok, dim3((n_prot + 255) / 256), dim3(256), 0, ctx->stream, d_nnodes, d_ntok, n_prot, ctx->df);
+  HIPCHK(hipGetLastError());
+  return PST_OK;
+}
+
+int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,
+                 int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
+  if (!ctx) return PST_E_INVALID;
+  ctx->err.clear();
+  int rc = validate(ctx, offsets, n_prot);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t R = offsets[n_prot];
+  rc = ensure_workspace(ctx, R, n_prot);
+  if (rc) return rc;
+  auto& w = ctx->w;
+  HIPCHK(hipMemcpyAsync(w.pos, atom_pos, sizeof(double) * 111 * R, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(w.flags, atom_flags, 37 * R, hipMemcpyHostToDevice, ctx->stream));
+  rc = run(ctx, w.pos, w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_ntok, dim3((n_prot + 255) / 256), dim3(256), 0, ctx->stream, w.n_nodes, w.n_tok, n_prot, ctx->df);
+  HIPCHK(hipMemcpyAsync(tokens_out, w.tokens, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, ctx->stream));
+  if (n_tokens_out)
+    HIPCHK(hipMemcpyAsync(n_tokens_out, w.n_tok, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
+  if (n_nodes_out)
+    HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return PST_OK;
+}
+
+int pst_aux(pst_ctx* ctx, float* bounded, float* quantize, float* pre_proj) {
+  if (!ctx || ctx->last_R == 0) return PST_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const int64_t R = ctx->last_R;
+  const int D = ctx->D;
+  if (bounded || quantize) {
+    std::vector<float> b8((size_t)R * 8), q8((size_t)R * 8);
+    HIPCHK(hipMemcpy(b8.data(), ctx->w.bounded, sizeof(float) * 8 * R, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(q8.data(), ctx->w.quant, sizeof(float) * 8 * R, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < R; ++i)
+      for (int d = 0; d < D; ++d) {
+        if (bounded) bounded[i * D + d] = b8[i * 8 + d];
+        if (quantize) quantize[i * D + d] = q8[i * 8 + d];
+      }
+  }
+  if (pre_proj) HIPCHK(hipMemcpy(pre_proj, ctx->w.pre_proj, sizeof(float) * 128 * R, hipMemcpyDeviceToHost));
+  return PST_OK;
+}
+
+int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t* argmin) {
+  return fail(ctx, PST_E_INVALID, "pst_codebook_aux: not implemented in this build");
+}
+
+int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes) {
+  if (!ctx || ctx->last_R == 0) return PST_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const int64_t Rp = ctx->last_Rpad;
+  const void* src = nullptr;
+  size_t need = 0;
+  std::vector<float> tmp;
+  if (which >= 0 && which <= 3) {  // node features after init embed / layer `which` (perm → natural)
+    if (which == 0) return fail(ctx, PST_E_INVALID, "init embedding is a table (not kept per call)");
+    const float* d = which == 3 ? ctx->w.h0 : ctx->dbg[which - 1];
+    if (!d) return fail(ctx, PST_E_INVALID, "intermediate layers need PST_DEBUG=1 at context creation");
+    tmp.resize((size_t)Rp * 128);
+    HIPCHK(hipMemcpy(tmp.data(), d, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
+    need = (size_t)ctx->last_R * 128 * sizeof(float);
+    if (bytes < need) return fail(ctx, PST_E_INVALID, "debug buffer too small");
+    float* o = (float*)out;
+    for (int64_t i = 0; i < ctx->last_R; ++i)
+      for (int h = 0; h < 2; ++h)
+        for (int M = 0; M < 4; ++M)
+          for (int r = 0; r < 16; ++r) o[i * 128 + tile_channel(h, M, r)] = tmp[i * 128 + h * 64 + M * 16 + r];
+    return PST_OK;
+  }
+  if (which == 10) {
+    src = ctx->w.feat;
+    need = (size_t)ctx->last_R * KNN * 32 * sizeof(float);
+  } else if (which == 11) {
+    src = ctx->w.senders;
+    need = (size_t)ctx->last_R * KNN * sizeof(int32_t);
+  } else if (which == 12) {
+    src = ctx->w.deg;
+    need = (size_t)ctx->last_R * sizeof(int32_t);
+  } else {
+    return fail(ctx, PST_E_INVALID, "unknown debug id");
+  }
+  if (bytes < need) return fail(ctx, PST_E_INVALID, "debug buffer too small");
+  HIPCHK(hipMemcpy(out, src, need, hipMemcpyDeviceToHost));
+  return PST_OK;
+}
+
+}  // extern "C"

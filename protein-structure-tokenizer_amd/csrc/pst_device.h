@@ -1,0 +1,315 @@
+// pst_device.h — device-side building blocks of libpst (gfx950 / CDNA4).
+//
+// 1. Canonical numerics. Every operation is a fixed sequence of IEEE-754 ops
+//    (fmaf, +, *, /, sqrtf are correctly rounded on gfx950; compiled with -ffp-contract=off),
+//    so results are bit-identical to any CPU implementation of the same sequence.
+// 2. The wave tile: 32 columns (edges, nodes or tokens — one per lane&31) x 128 channels held
+//    as four 32x32 f32 MFMA accumulators. Lane l = (col = l&31, half h = l>>5) owns channels
+//    c = 32*M + (r&3) + 8*(r>>2) + 4*h of accumulator M, register r. An accumulator tile feeds
+//    the next v_mfma_f32_32x32x2_f32 as its B operand register by register (k-step (M, r) =
+//    channel pair (c, c+4)), so a chain of Linear layers never leaves registers; the dot
+//    products are fmaf chains in the "pi8" k order 0,4,1,5,2,6,3,7 per block of 8 channels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pst {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------ canonical f32 math
+__device__ __forceinline__ float c_tanh(float a) {
+  const float clamp = 7.99881172180175781f;
+  float x = fminf(fmaxf(a, -clamp), clamp);
+  float x2 = x * x;
+  float p = __builtin_fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = __builtin_fmaf(x2, p, -8.60467152213735e-11f);
+  p = __builtin_fmaf(x2, p, 5.12229709037114e-08f);
+  p = __builtin_fmaf(x2, p, 1.48572235717979e-05f);
+  p = __builtin_fmaf(x2, p, 6.37261928875436e-04f);
+  p = __builtin_fmaf(x2, p, 4.89352455891786e-03f);
+  p = x * p;
+  float q = __builtin_fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = __builtin_fmaf(x2, q, 2.26843463243900e-03f);
+  q = __builtin_fmaf(x2, q, 4.89352518554385e-03f);
+  float r = p / q;
+  return fabsf(a) < 0.0004f ? a : r;
+}
+
+__device__ __forceinline__ float c_gelu(float x) {
+  float x3 = x * (x * x);
+  float inner = 0.797884583473205566f * (x + 0.0447149984538555145f * x3);
+  float cdf = 0.5f * (1.0f + c_tanh(inner));
+  return x * cdf;
+}
+
+__device__ __forceinline__ float c_ldexpf(float v, int n) {
+  if (n < -126) {
+    v = v * __uint_as_float((uint32_t)(-126 + 127) << 23);
+    n += 126;
+    if (n < -126) n = -126;
+  }
+  if (n > 127) n = 127;
+  return v * __uint_as_float((uint32_t)(n + 127) << 23);
+}
+
+__device__ __forceinline__ float c_exp(float x) {
+  if (x > 88.7228394f) return __builtin_inff();
+  if (x < -103.972084f) return 0.0f;
+  float n = rintf(x * 1.44269502f);
+  float r = __builtin_fmaf(n, -0.693145752f, x);
+  r = __builtin_fmaf(n, -1.42860677e-6f, r);
+  float p = 1.98756912e-4f;
+  p = __builtin_fmaf(p, r, 1.39819994e-3f);
+  p = __builtin_fmaf(p, r, 8.33345205e-3f);
+  p = __builtin_fmaf(p, r, 4.16657962e-2f);
+  p = __builtin_fmaf(p, r, 1.66666655e-1f);
+  p = __builtin_fmaf(p, r, 5.00000012e-1f);
+  float y = __builtin_fmaf(p, r * r, r) + 1.0f;
+  return c_ldexpf(y, (int)n);
+}
+
+__device__ __forceinline__ float c_sigmoid(float x) { return 1.0f / (1.0f + c_exp(-x)); }
+
+// ------------------------------------------------------------------ canonical f64 math
+__device__ __forceinline__ double c_ldexp64(double v, int n) {
+  if (n < -1022) {
+    v = v * __longlong_as_double((long long)(-1022 + 1023) << 52);
+    n += 1022;
+    if (n < -1022) n = -1022;
+  }
+  if (n > 1023) n = 1023;
+  return v * __longlong_as_double((long long)(n + 1023) << 52);
+}
+
+__device__ __forceinline__ double c_exp64(double x) {
+  if (x > 709.782712893384) return __builtin_inf();
+  if (x < -745.2) return 0.0;
+  double n = rint(x * 1.4426950408889634);
+  double r = __builtin_fma(n, -6.93147180369123816490e-01, x);
+  r = __builtin_fma(n, -1.90821492927058770002e-10, r);
+  double p = 1.0 / 6227020800.0;
+  p = __builtin_fma(p, r, 1.0 / 479001600.0);
+  p = __builtin_fma(p, r, 1.0 / 39916800.0);
+  p = __builtin_fma(p, r, 1.0 / 3628800.0);
+  p = __builtin_fma(p, r, 1.0 / 362880.0);
+  p = __builtin_fma(p, r, 1.0 / 40320.0);
+  p = __builtin_fma(p, r, 1.0 / 5040.0);
+  p = __builtin_fma(p, r, 1.0 / 720.0);
+  p = __builtin_fma(p, r, 1.0 / 120.0);
+  p = __builtin_fma(p, r, 1.0 / 24.0);
+  p = __builtin_fma(p, r, 1.0 / 6.0);
+  p = __builtin_fma(p, r, 0.5);
+  double y = __builtin_fma(p, r * r, r) + 1.0;
+  return c_ldexp64(y, (int)n);
+}
+
+// ------------------------------------------------------------------ wave tile
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// channel held by (half h, accumulator M, register r)
+__host__ __device__ constexpr int tile_channel(int h, int M, int r) {
+  return 32 * M + (r & 3) + 8 * (r >> 2) + 4 * h;
+}
+
+struct Tile {
+  f32x16 m[4];
+};
+
+// Buffer-resource loads/stores: wave-uniform base in SGPRs, per-lane byte offset in one VGPR,
+// per-instruction constant offset in an SGPR. Keeps unrolled fragment streams from
+// materialising one 64-bit address per k-step (which spilled the first version).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ float buf_load1(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t rs, int voff, int soff, float a, float b, float c,
+                                           float d) {
+  u32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
+}
+
+__device__ __forceinline__ void tile_zero(Tile& t) {
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t.m[M][r] = 0.0f;
+}
+
+// Load a 128-channel row stored in "perm" order (perm[h*64 + M*16 + r] = v[tile_channel]).
+// `row` is this lane's row base; the lane reads its 64 floats (256 B) contiguously.
+__device__ __forceinline__ void tile_load_perm(Tile& t, const float* __restrict__ row) {
+  const float4* p = reinterpret_cast<const float4*>(row + (lane_id() >> 5) * 64);
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 v = p[M * 4 + q];
+      t.m[M][4 * q + 0] = v.x;
+      t.m[M][4 * q + 1] = v.y;
+      t.m[M][4 * q + 2] = v.z;
+      t.m[M][4 * q + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void tile_store_perm(const Tile& t, float* __restrict__ row) {
+  float4* p = reinterpret_cast<float4*>(row + (lane_id() >> 5) * 64);
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      p[M * 4 + q] = make_float4(t.m[M][4 * q], t.m[M][4 * q + 1], t.m[M][4 * q + 2], t.m[M][4 * q + 3]);
+}
+
+// Blocked tile storage: [16 quads][64 lanes][4] floats (16 KB), fully coalesced.
+// `blk` must be wave-uniform.
+__device__ __forceinline__ void tile_load_blk(Tile& t, const float* __restrict__ blk) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(blk);
+  const int vo = lane_id() * 16;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 v = buf_load4(rs, vo, (M * 4 + q) * 1024);
+      t.m[M][4 * q + 0] = v.x;
+      t.m[M][4 * q + 1] = v.y;
+      t.m[M][4 * q + 2] = v.z;
+      t.m[M][4 * q + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void tile_store_blk(const Tile& t, float* __restrict__ blk) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(blk);
+  const int vo = lane_id() * 16;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      buf_store4(rs, vo, (M * 4 + q) * 1024, t.m[M][4 * q], t.m[M][4 * q + 1], t.m[M][4 * q + 2], t.m[M][4 * q + 3]);
+}
+
+// acc += X · W over K = 128 channels (64 k-steps), four output accumulators.
+// Wf: A fragments, [64 k-steps][64 lanes] float4 (one f32 per output accumulator).
+// The fragment stream runs GEMM_DEPTH k-steps ahead in a register ring; a scheduling
+// barrier per k-step keeps the compiler from hoisting the whole stream (register spills).
+#ifndef GEMM_DEPTH
+#define GEMM_DEPTH 4
+#endif
+__device__ __forceinline__ void tile_gemm(Tile& acc, const Tile& X, const float4* __restrict__ Wf) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
+  const int vo = lane_id() * 16;
+  float4 ring[GEMM_DEPTH];
+#pragma unroll
+  for (int i = 0; i < GEMM_DEPTH; ++i) ring[i] = buf_load4(rs, vo, i * 1024);
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    float4 a = ring[t % GEMM_DEPTH];
+    if (t + GEMM_DEPTH < 64) ring[t % GEMM_DEPTH] = buf_load4(rs, vo, (t + GEMM_DEPTH) * 1024);
+    float b = X.m[t / 16][t % 16];
+    acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b, acc.m[0], 0, 0, 0);
+    acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b, acc.m[1], 0, 0, 0);
+    acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b, acc.m[2], 0, 0, 0);
+    acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b, acc.m[3], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// acc(one 32-output accumulator) += X · W, W: [64 k-steps][64 lanes] f32 (K = 128)
+__device__ __forceinline__ void tile_gemm_narrow(f32x16& acc, const Tile& X, const float* __restrict__ Wf) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
+  const int vo = lane_id() * 4;
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(buf_load1(rs, vo, t * 256), X.m[t / 16][t % 16], acc, 0, 0, 0);
+  }
+}
+
+// elementwise helpers on a perm-ordered vector held in LDS/global (this lane's 64 values)
+__device__ __forceinline__ void tile_add_vec(Tile& t, const float* __restrict__ vperm) {
+  const float4* p = reinterpret_cast<const float4*>(vperm + (lane_id() >> 5) * 64);
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __builtin_amdgcn_sched_barrier(0);
+      float4 v = p[M * 4 + q];
+      t.m[M][4 * q + 0] = t.m[M][4 * q + 0] + v.x;
+      t.m[M][4 * q + 1] = t.m[M][4 * q + 1] + v.y;
+      t.m[M][4 * q + 2] = t.m[M][4 * q + 2] + v.z;
+      t.m[M][4 * q + 3] = t.m[M][4 * q + 3] + v.w;
+    }
+}
+
+__device__ __forceinline__ void tile_gelu(Tile& t) {
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t.m[M][r] = c_gelu(t.m[M][r]);
+}
+
+__device__ __forceinline__ void tile_relu(Tile& t) {
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t.m[M][r] = t.m[M][r] > 0.0f ? t.m[M][r] : 0.0f;
+}
+
+__device__ __forceinline__ void tile_add(Tile& a, const Tile& b) {
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a.m[M][r] = a.m[M][r] + b.m[M][r];
+}
+
+__device__ __forceinline__ float partner(float v) { return __shfl_xor(v, 32, 64); }
+
+// split sum (canonical): this lane's 64 channels in order, plus the partner half's sum
+__device__ __forceinline__ float tile_split_sum(const Tile& t) {
+  float s = 0.0f;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s = s + t.m[M][r];
+  return s + partner(s);
+}
+
+// LayerNorm / MaskedLayerNorm (mask 1) over the 128 channels of each column, in place.
+// scale/offset are perm-ordered 128-vectors.
+__device__ __forceinline__ void tile_layer_norm(Tile& t, const float* __restrict__ scale,
+                                                const float* __restrict__ offset) {
+  float mean = tile_split_sum(t) / 128.0f;
+  float s = 0.0f;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float d = t.m[M][r] - mean;
+      s = s + d * d;
+    }
+  float var = (s + partner(s)) / 128.0f;
+  float rs = 1.0f / sqrtf(var + 1e-5f);
+  const float4* ps = reinterpret_cast<const float4*>(scale + (lane_id() >> 5) * 64);
+  const float4* po = reinterpret_cast<const float4*>(offset + (lane_id() >> 5) * 64);
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __builtin_amdgcn_sched_barrier(0);
+      float4 sc = ps[M * 4 + q], of = po[M * 4 + q];
+      float scv[4] = {sc.x, sc.y, sc.z, sc.w}, ofv[4] = {of.x, of.y, of.z, of.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float inv = scv[i] * rs;
+        t.m[M][4 * q + i] = inv * (t.m[M][4 * q + i] - mean) + ofv[i];
+      }
+    }
+}
+
+}  // namespace pst

@@ -1,0 +1,124 @@
+// pst_kernels.h — kernel argument blocks and launchers (host <-> device contract of libpst).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pst {
+
+struct PrepArgs {
+  const double* pos;       // [R,37,3]
+  const uint8_t* flags;    // [R,37]
+  const int64_t* offsets;  // [B+1]
+  int32_t* n_nodes;        // [B]
+  int32_t* node_local;     // [R_pad] (-1 = gap / padding)
+  int32_t* node_prot;      // [R_pad]
+  double* frame;           // [R_pad,9] rows n,u,v
+  double* cen;             // [R_pad,3]
+  double* ca;              // [R_pad,3]
+};
+
+struct KnnArgs {
+  int64_t n_slots;  // R_pad
+  const int64_t* offsets;
+  const int32_t* n_nodes;
+  const int32_t* node_local;
+  const int32_t* node_prot;
+  const double* frame;
+  const double* cen;
+  const double* ca;
+  int32_t* senders;  // [R_pad*50] global slot of the sender
+  int32_t* deg;      // [R_pad] valid slots per receiver
+  float* feat;       // [R_pad*50, 32]
+};
+
+struct MlpW {  // one 3-layer MLP on the edge tile; w*: A fragments [64][64] float4, b*: perm
+  const float4* w0;  // rows 256..383 of the [384,128] first layer (the edge part)
+  const float* b0;
+  const float4* w1;
+  const float* b1;
+  const float4* w2;
+  const float* b2;
+};
+
+struct MpnnArgs {
+  int64_t n_tasks;  // R_pad / 32
+  const int32_t* senders;
+  const int32_t* deg;
+  const int32_t* node_local;
+  // layer 0 only
+  const float* feat;       // graph edge features
+  const float* Ttab;       // [1023][128] perm: edge PE projection
+  const float4* W_embed;   // [16][64] float4: init_edge_embed rows 128..154 (+zero pad)
+  const float* b_embed;    // perm
+  const float* PM0;        // [512][256] perm: h0 · msg0 W[0:128] | W[128:256]
+  const float* h0tab;      // [512][128] perm: init_node_embed(node PE)
+  // layers >= 1
+  const float* e_in;       // blocked edge features of the previous layer
+  const float* P_in;       // [R_pad][512] perm projections [E_s | E_r | M_s | M_r]
+  const float* h_in;       // [R_pad][128] perm
+  MlpW edge;               // edge MLP of layer-1
+  const float* edge_ln_s;
+  const float* edge_ln_o;
+  // this layer
+  MlpW msg;
+  const float* ln0_s;
+  const float* ln0_o;
+  const float* ln1_s;
+  const float* ln1_o;
+  const float4* ff_w1;  // [4 chunks][64][64]
+  const float* ff_b1;   // [4][128] perm
+  const float4* ff_w2;  // [4 chunks][64][64]
+  const float* ff_b2;
+  const float4* proj_w;  // [4][64][64]: next kernel's E_s, E_r, M_s, M_r projections (or null)
+  // outputs
+  float* e_out;  // blocked (null for the last layer)
+  float* h_out;
+  float* P_out;  // null for the last layer
+};
+
+struct DownBlockW {
+  const float *qn_s, *qn_o, *dn_s, *dn_o;
+  const float4 *wq, *wk, *wv, *wg, *wo;
+  const float *gb, *ob;
+  const float *rt_ln_s, *rt_ln_o;
+  const float4* rt_w1;  // [2][64][64]
+  const float* rt_b1;   // [2][128]
+  const float4* rt_w2;  // [2][64][64]
+  const float* rt_b2;
+  const float *ot_ln_s, *ot_ln_o;
+  const float4* ot_w1;
+  const float* ot_b1;
+  const float4* ot_w2;
+  const float* ot_b2;
+};
+
+struct DownArgs {
+  int32_t n_tiles;
+  const int32_t* tile_prot;
+  const int32_t* tile_t0;
+  const int64_t* offsets;
+  const int32_t* n_nodes;
+  const float* RPE;  // [max_out][128] perm
+  float* o_buf;      // [R_pad][128] perm: original track (h3, updated in place)
+  float* r_buf;      // [R_pad][128] perm: resampled track
+  float* v_buf;      // [R_pad][128] perm: values (DF > 1)
+  DownBlockW blk[3];
+  const float* down_w;  // [64][64] f32 narrow fragments
+  const float* down_b;  // [8]
+  int32_t D;
+  float fsq_half[8], fsq_off[8], fsq_shift[8];
+  int32_t fsq_L[8], fsq_basis[8];
+  uint32_t* tokens_out;  // [R] (raw-offset layout)
+  float* bounded_out;    // [R,8]
+  float* quant_out;      // [R,8]
+  float* pre_proj_out;   // [R,128]
+};
+
+void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st);
+void launch_knn(const KnnArgs& a, hipStream_t st);
+void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st);
+void launch_down(int df, const DownArgs& a, hipStream_t st);
+void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, float* Y, int ldy,
+                       hipStream_t st);
+
+}  // namespace pst

@@ -1,0 +1,662 @@
+// pst_kernels.hip — HIP kernels of the tokenize path for gfx950 (MI355X).
+//
+// Pipeline per batch (one stream, 6 launches, all data resident in HBM):
+//   k_prep       block/protein: backbone filter + compaction, frames, centroids, CA
+//                (preprocessing.py:69-149, quat_affine.py:406-522)
+//   k_knn        wave/receiver: float64 cdist row, ordered k-NN selection, 27 edge features
+//                (protein_utils.py:636-749; padding semantics preprocessing.py:191-271)
+//   k_mpnn<0..2> wave/32 receivers (1600 edge slots = 50 MFMA blocks of 32 edges): fused
+//                edge update of layer l-1 + message MLP of layer l + ordered segment sum +
+//                node update (masked LN, 128->512->128 FFN, masked LN) + the next layer's node
+//                projections (gnn_layers.py:325-438). Edge features never leave registers
+//                between Linear layers; e is stored once per layer in a coalesced blocked
+//                layout.
+//   k_down<DF>   wave/32 tokens: cross-attention downsampler (3 blocks), spherical norm,
+//                down_proj and FSQ (modules.py:427-636, model.py:169-174, quantize.py:175-209)
+// See pst_device.h for the wave-tile layout and DESIGN.md for the numerics contract.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pst_device.h"
+#include "pst_kernels.h"
+
+namespace pst {
+
+#define NATOM 37
+#define KNN 50
+
+// ---------------------------------------------------------------------------- k_prep
+struct Frame {
+  double u[3], v[3], n[3];
+};
+
+__device__ __forceinline__ void make_frame(const double* N, const double* CA, const double* C, double* out) {
+  double nx = N[0] + (-CA[0]), ny = N[1] + (-CA[1]), nz = N[2] + (-CA[2]);
+  double cx = C[0] + (-CA[0]), cy = C[1] + (-CA[1]), cz = C[2] + (-CA[2]);
+  double s1 = sqrt(1e-20 + cx * cx + cy * cy);
+  double sin_c1 = -cy / s1, cos_c1 = cx / s1;
+  double c1[3][3] = {{cos_c1, -sin_c1, 0.0}, {sin_c1, cos_c1, 0.0}, {0.0, 0.0, 1.0}};
+  double s2 = sqrt(1e-20 + cx * cx + cy * cy + cz * cz);
+  double sin_c2 = cz / s2, cos_c2 = sqrt(cx * cx + cy * cy) / s2;
+  double c2[3][3] = {{cos_c2, 0.0, sin_c2}, {0.0, 1.0, 0.0}, {-sin_c2, 0.0, cos_c2}};
+  double cr[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) cr[i][j] = c2[i][0] * c1[0][j] + c2[i][1] * c1[1][j] + c2[i][2] * c1[2][j];
+  double ry = cr[1][0] * nx + cr[1][1] * ny + cr[1][2] * nz;
+  double rz = cr[2][0] * nx + cr[2][1] * ny + cr[2][2] * nz;
+  double s3 = sqrt(1e-20 + ry * ry + rz * rz);
+  double sin_n = -rz / s3, cos_n = ry / s3;
+  double nr[3][3] = {{1.0, 0.0, 0.0}, {0.0, cos_n, -sin_n}, {0.0, sin_n, cos_n}};
+  double M[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) M[i][j] = nr[i][0] * cr[0][j] + nr[i][1] * cr[1][j] + nr[i][2] * cr[2][j];
+  // stored rows: [n | u | v] = [M2 | M0 | M1]  (basis_matrices order, protein_utils.py:717)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    out[k] = M[2][k];
+    out[3 + k] = M[0][k];
+    out[6 + k] = M[1][k];
+  }
+}
+
+__global__ __launch_bounds__(512) void k_prep(PrepArgs a) {
+  __shared__ int wave_cnt[8];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t off = a.offsets[b];
+  const int Rb = (int)(a.offsets[b + 1] - off);
+  bool keep = false;
+  if (tid < Rb) {
+    const uint8_t* fl = a.flags + (off + tid) * NATOM;
+    keep = (fl[0] & 1) && (fl[1] & 1) && (fl[2] & 1) && (fl[4] & 1);  // N, CA, C, O gt_exists
+  }
+  unsigned long long m = __ballot(keep);
+  if (lane == 0) wave_cnt[w] = __popcll(m);
+  __syncthreads();
+  int base = 0, total = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (i < w) base += wave_cnt[i];
+    total += wave_cnt[i];
+  }
+  const int loc = base + __popcll(m & ((1ull << lane) - 1ull));
+  if (tid == 0) a.n_nodes[b] = total;
+  if (keep) {
+    const int64_t slot = off + loc;
+    const double* P = a.pos + (off + tid) * NATOM * 3;
+    const uint8_t* fl = a.flags + (off + tid) * NATOM;
+    make_frame(P + 0, P + 3, P + 6, a.frame + slot * 9);
+    double sx = 0.0, sy = 0.0, sz = 0.0;
+    int cnt = 0;
+    for (int at = 0; at < NATOM; ++at)
+      if ((fl[at] & 3) == 3) {  // gt_exists & atom_exists (preprocessing.py:72)
+        if (cnt == 0) { sx = P[3 * at]; sy = P[3 * at + 1]; sz = P[3 * at + 2]; }
+        else { sx += P[3 * at]; sy += P[3 * at + 1]; sz += P[3 * at + 2]; }
+        ++cnt;
+      }
+    a.cen[slot * 3 + 0] = sx / cnt;
+    a.cen[slot * 3 + 1] = sy / cnt;
+    a.cen[slot * 3 + 2] = sz / cnt;
+    a.ca[slot * 3 + 0] = P[3];
+    a.ca[slot * 3 + 1] = P[4];
+    a.ca[slot * 3 + 2] = P[5];
+    a.node_local[slot] = loc;
+    a.node_prot[slot] = b;
+  }
+  if (tid >= total && tid < Rb) {  // gap slots left by filtered residues
+    a.node_local[off + tid] = -1;
+    a.node_prot[off + tid] = b;
+  }
+}
+
+// ---------------------------------------------------------------------------- k_knn
+__device__ __forceinline__ double dot3(const double* b, const double* x) {
+  // numpy einsum's evaluation order for the 3-term contraction (protein_utils.py:722-733)
+  return ((0.0 + b[0] * x[0]) + b[2] * x[2]) + b[1] * x[1];
+}
+
+__device__ void edge_features(const double* fr_r, const double* fr_s, const double* ca_r,
+                              const double* ca_s, double dist, float* __restrict__ out) {
+  float f[32];
+  double d2 = dist * dist;
+  double ls = 1.0;
+#pragma unroll
+  for (int j = 0; j < 15; ++j) {
+    f[j] = (float)c_exp64(-d2 / ls);
+    ls *= 1.5;
+  }
+  double diff[3] = {ca_s[0] - ca_r[0], ca_s[1] - ca_r[1], ca_s[2] - ca_r[2]};
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double* row = fr_r + 3 * j;  // rows n, u, v of the receiver basis
+    f[15 + j] = (float)dot3(row, diff);
+    f[18 + j] = (float)dot3(row, fr_s + 0);
+    f[21 + j] = (float)dot3(row, fr_s + 3);
+    f[24 + j] = (float)dot3(row, fr_s + 6);
+  }
+#pragma unroll
+  for (int j = 27; j < 32; ++j) f[j] = 0.0f;
+  float4* o = reinterpret_cast<float4*>(out);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+}
+
+__device__ __forceinline__ bool lex_less(double d1, int s1, double d2, int s2) {
+  return d1 < d2 || (d1 == d2 && s1 < s2);
+}
+
+__device__ __forceinline__ double cen_dist(const double* cen, int64_t r, int64_t s) {
+  double dx = cen[r * 3] - cen[s * 3], dy = cen[r * 3 + 1] - cen[s * 3 + 1], dz = cen[r * 3 + 2] - cen[s * 3 + 2];
+  return sqrt(dx * dx + dy * dy + dz * dz);
+}
+
+// rank-cc neighbour (self included) of local receiver rr, by counting (n < k branch only)
+__device__ int rank_select(const double* cen, int64_t base, int n, int rr, int cc, double* dsel) {
+  for (int s = 0; s < n; ++s) {
+    double ds = cen_dist(cen, base + rr, base + s);
+    int rank = 0;
+    for (int q = 0; q < n; ++q) {
+      double dq = cen_dist(cen, base + rr, base + q);
+      rank += lex_less(dq, q, ds, s);
+    }
+    if (rank == cc) { *dsel = ds; return s; }
+  }
+  *dsel = 0.0;
+  return rr;
+}
+
+__global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= a.n_slots) return;
+  const int loc = a.node_local[g];
+  int32_t* snd = a.senders + g * KNN;
+  float* feat = a.feat + g * KNN * 32;
+  if (loc < 0) {  // gap / padding slot: self edges, zero features, degree 0
+    if (lane < KNN) {
+      snd[lane] = (int32_t)g;
+      float4* o = reinterpret_cast<float4*>(feat + lane * 32);
+      for (int q = 0; q < 8; ++q) o[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (lane == 0) a.deg[g] = 0;
+    return;
+  }
+  const int b = a.node_prot[g];
+  const int64_t base = a.offsets[b];
+  const int n = a.n_nodes[b];
+  // candidate distances (float64, scipy cdist order), 8 per lane
+  double d[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    int s = lane + 64 * i;
+    d[i] = s < n ? cen_dist(a.cen, g, base + s) : __builtin_inf();
+  }
+  const int keep = n <= KNN ? n : KNN + 1;
+  const int drop = n <= KNN ? 0 : 1;  // column 0 (self) dropped when n > k (protein_utils.py:700)
+  unsigned taken = 0;
+  int my_s = -1;
+  double my_d = 0.0;
+  for (int t = 0; t < keep; ++t) {
+    double bd = __builtin_inf();
+    int bs = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int s = lane + 64 * i;
+      bool ok = s < n && !((taken >> i) & 1u);
+      if (ok && lex_less(d[i], s, bd, bs)) { bd = d[i]; bs = s; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      double od = __shfl_xor(bd, o, 64);
+      int os = __shfl_xor(bs, o, 64);
+      if (lex_less(od, os, bd, bs)) { bd = od; bs = os; }
+    }
+    if ((bs & 63) == lane) taken |= 1u << (bs >> 6);
+    if (t - drop == lane) { my_s = bs; my_d = bd; }
+  }
+  const int deg = n <= KNN ? n : KNN;
+  if (lane == 0) a.deg[g] = deg;
+  if (lane < KNN) {
+    if (n >= KNN) {
+      snd[lane] = (int32_t)(base + my_s);
+      edge_features(a.frame + g * 9, a.frame + (base + my_s) * 9, a.ca + g * 3, a.ca + (base + my_s) * 3, my_d,
+                    feat + lane * 32);
+    } else {
+      // n < k (preprocessing.py:229-260): senders stay per-row, features keep the n*n order
+      snd[lane] = lane < n ? (int32_t)(base + my_s) : (int32_t)g;
+      int64_t f = (int64_t)loc * KNN + lane;
+      if (f < (int64_t)n * n) {
+        int rr = (int)(f / n), cc = (int)(f % n);
+        double ds;
+        int s = rank_select(a.cen, base, n, rr, cc, &ds);
+        edge_features(a.frame + (base + rr) * 9, a.frame + (base + s) * 9, a.ca + (base + rr) * 3,
+                      a.ca + (base + s) * 3, ds, feat + lane * 32);
+      } else {
+        float4* o = reinterpret_cast<float4*>(feat + lane * 32);
+        for (int q = 0; q < 8; ++q) o[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- k_mpnn
+// perm position of channel c (inverse of tile_channel)
+__device__ __forceinline__ int perm_pos(int c) {
+  int h = (c >> 2) & 1, M = c >> 5, cc = c & 31;
+  int r = (cc & 3) + 4 * (cc >> 3);
+  return h * 64 + M * 16 + r;
+}
+
+__device__ __forceinline__ void tile_add_rows(Tile& acc, const float* __restrict__ a_row, const float* __restrict__ b_row) {
+  Tile t;
+  tile_load_perm(acc, a_row);
+  tile_load_perm(t, b_row);
+  tile_add(acc, t);
+}
+
+// 3-layer edge MLP starting from acc = init (already Ps + Pr): acc <- MLP(init, X)
+__device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
+  tile_gemm(acc, X, W.w0);
+  tile_add_vec(acc, W.b0);
+  tile_gelu(acc);
+  Tile a2;
+  tile_zero(a2);
+  tile_gemm(a2, acc, W.w1);
+  tile_add_vec(a2, W.b1);
+  tile_gelu(a2);
+  tile_zero(acc);
+  tile_gemm(acc, a2, W.w2);
+  tile_add_vec(acc, W.b2);
+}
+
+template <int LAYER>
+__global__ __launch_bounds__(256, 2) void k_mpnn(MpnnArgs a) {
+  __shared__ float lds_scratch[4][32 * 32];
+  __shared__ float lds_agg[4][32 * 128];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t task = (int64_t)blockIdx.x * 4 + w;
+  if (task >= a.n_tasks) return;
+  const int64_t g0 = task * 32;
+  float* scratch = lds_scratch[w];
+  float* aggl = lds_agg[w];
+  const int c = lane & 31, part = lane >> 5;
+  for (int i = lane; i < 32 * 128; i += 64) aggl[i] = 0.0f;
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int blk = 0; blk < 50; ++blk) {
+    const int te = 32 * blk + (lane & 31);
+    const int rl = te / 50;
+    const int64_t g = g0 + rl;
+    const int64_t E = g * KNN + (te - 50 * rl);
+    const int64_t s = a.senders[E];
+    const int64_t eblk = (task * 50 + blk) * 4096;
+    Tile e;
+    if (LAYER == 0) {
+      // init_edge_embed: chain from T[s-r] over the 27 (+5 zero) features, + bias
+      int lr = a.node_local[g], ls = a.node_local[s];
+      lr = lr < 0 ? 0 : lr;
+      ls = ls < 0 ? lr : ls;
+      tile_load_perm(e, a.Ttab + (int64_t)(ls - lr + 511) * 128);
+      const float4* fp = reinterpret_cast<const float4*>(a.feat + E * 32 + 4 * (lane >> 5));
+      float x[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 v = fp[2 * q];
+        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+      }
+      const float4* wf = a.W_embed + lane;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float4 wa = wf[r * 64];
+        e.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, x[r], e.m[0], 0, 0, 0);
+        e.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, x[r], e.m[1], 0, 0, 0);
+        e.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, x[r], e.m[2], 0, 0, 0);
+        e.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, x[r], e.m[3], 0, 0, 0);
+      }
+      tile_add_vec(e, a.b_embed);
+    } else {
+      // edge update of layer LAYER-1: e = LN(e + MLP([h_s | h_r | e]))
+      Tile ein;
+      tile_load_blk(ein, a.e_in + eblk);
+      Tile acc;
+      tile_add_rows(acc, a.P_in + s * 512 + 0, a.P_in + g * 512 + 128);
+      mlp3(acc, ein, a.edge);
+      tile_load_blk(e, a.e_in + eblk);
+      tile_add(e, acc);
+      tile_layer_norm(e, a.edge_ln_s, a.edge_ln_o);
+    }
+    if (a.e_out) tile_store_blk(e, a.e_out + eblk);
+    // message MLP of layer LAYER
+    Tile m;
+    if (LAYER == 0) {
+      int lr = a.node_local[g], ls = a.node_local[s];
+      lr = lr < 0 ? 0 : lr;
+      ls = ls < 0 ? lr : ls;
+      tile_add_rows(m, a.PM0 + (int64_t)ls * 256 + 0, a.PM0 + (int64_t)lr * 256 + 128);
+    } else {
+      tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
+    }
+    mlp3(m, e, a.msg);
+    // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order)
+    const int rA = (32 * blk) / 50;
+    const int lastA = 50 * (rA + 1) - 1 - 32 * blk;  // block-local index of rA's last edge
+    const int degA = a.deg[g0 + rA];
+    const int degB = rA + 1 < 32 ? a.deg[g0 + rA + 1] : 0;
+    const int j0 = 32 * blk - 50 * rA;  // slot of the block's edge 0 in rA
+#pragma unroll
+    for (int M = 0; M < 4; ++M) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int ch = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        scratch[ch * 32 + ((lane & 31) ^ ch)] = m.m[M][r];
+      }
+      __builtin_amdgcn_wave_barrier();
+      float acc = part == 0 ? carry[M] : 0.0f;
+      for (int ee = 0; ee < 32; ++ee) {
+        bool in = part == 0 ? (ee <= lastA && j0 + ee < degA) : (ee > lastA && ee - lastA - 1 < degB);
+        float v = scratch[c * 32 + (ee ^ c)];
+        if (in) acc = acc + v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      float other = __shfl_xor(acc, 32, 64);
+      if (lastA <= 31) {
+        if (part == 0) aggl[rA * 128 + perm_pos(32 * M + c)] = acc;
+        carry[M] = lastA < 31 ? other : 0.0f;
+      } else {
+        carry[M] = acc;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // ---------------- node update for the 32 receivers (lane&31 = receiver)
+  const int64_t gl = g0 + (lane & 31);
+  Tile x;
+  {
+    Tile ag;
+    tile_load_perm(ag, aggl + (lane & 31) * 128);
+    if (LAYER == 0) {
+      int lr = a.node_local[gl];
+      tile_load_perm(x, a.h0tab + (int64_t)(lr < 0 ? 0 : lr) * 128);
+    } else {
+      tile_load_perm(x, a.h_in + gl * 128);
+    }
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x.m[M][r] = x.m[M][r] + ag.m[M][r] / 50.0f;
+  }
+  tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0
+  Tile out;
+  tile_zero(out);
+  for (int ck = 0; ck < 4; ++ck) {
+    Tile hid;
+    tile_zero(hid);
+    tile_gemm(hid, x, a.ff_w1 + ck * 64 * 64);
+    tile_add_vec(hid, a.ff_b1 + ck * 128);
+    tile_gelu(hid);
+    tile_gemm(out, hid, a.ff_w2 + ck * 64 * 64);
+  }
+  tile_add_vec(out, a.ff_b2);
+  tile_add(x, out);
+  tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
+  tile_store_perm(x, a.h_out + gl * 128);
+  if (a.P_out) {
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+      Tile pr;
+      tile_zero(pr);
+      tile_gemm(pr, x, a.proj_w + p * 64 * 64);
+      tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- k_down
+template <int DF>
+__global__ __launch_bounds__(256) void k_down(DownArgs a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tile_id = blockIdx.x * 4 + w;
+  if (tile_id >= a.n_tiles) return;
+  const int b = a.tile_prot[tile_id];
+  const int t0 = a.tile_t0[tile_id];
+  const int64_t base = a.offsets[b];
+  const int T = a.n_nodes[b] / DF;
+  const int t = t0 + (lane & 31);
+  const bool valid = t < T;
+  const int tc = valid ? t : (T > 0 ? T - 1 : 0);  // clamp: invalid lanes recompute a real row
+  float* rrow = a.r_buf + (base + tc) * 128;
+  // resampled track init: sinusoidal PE of the token index (modules.py:488-500)
+  {
+    Tile r;
+    tile_load_perm(r, a.RPE + (int64_t)tc * 128);
+    if (valid) tile_store_perm(r, rrow);
+  }
+  for (int blk = 0; blk < 3; ++blk) {
+    const DownBlockW& W = a.blk[blk];
+    // ---- cross attention: v (and logits for DF > 1) from the original track
+    Tile wa;
+    if (DF == 1) {
+      Tile x;
+      tile_load_perm(x, a.o_buf + (base + tc) * 128);
+      tile_layer_norm(x, W.dn_s, W.dn_o);
+      tile_zero(wa);
+      tile_gemm(wa, x, W.wv);
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) wa.m[M][r] = wa.m[M][r] + 0.0f;  // fmaf(1, v, 0)
+    } else {
+      // q for the logits
+      Tile q;
+      tile_load_perm(q, rrow);
+      tile_layer_norm(q, W.qn_s, W.qn_o);
+      Tile qq;
+      tile_zero(qq);
+      tile_gemm(qq, q, W.wq);
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) qq.m[M][r] = qq.m[M][r] * 0.176776692f;
+      float logit[4][DF];
+      for (int p = 0; p < DF; ++p) {
+        Tile x;
+        tile_load_perm(x, a.o_buf + (base + (int64_t)tc * DF + p) * 128);
+        tile_layer_norm(x, W.dn_s, W.dn_o);
+        Tile kk;
+        tile_zero(kk);
+        tile_gemm(kk, x, W.wk);
+        Tile vv;
+        tile_zero(vv);
+        tile_gemm(vv, x, W.wv);
+        tile_store_perm(vv, a.v_buf + (base + (int64_t)tc * DF + p) * 128);
+#pragma unroll
+        for (int hd = 0; hd < 4; ++hd) {
+          float accl = 0.0f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float q0 = qq.m[hd][r], k0 = kk.m[hd][r];
+            float q1 = __shfl_xor(q0, 32, 64), k1 = __shfl_xor(k0, 32, 64);
+            if (lane >= 32) { float tq = q0; q0 = q1; q1 = tq; float tk = k0; k0 = k1; k1 = tk; }
+            accl = __builtin_fmaf(q0, k0, accl);  // channel f(r)      (half 0)
+            accl = __builtin_fmaf(q1, k1, accl);  // channel f(r) + 4  (half 1)
+          }
+          logit[hd][p] = accl;
+        }
+      }
+      float wgt[4][DF];
+#pragma unroll
+      for (int hd = 0; hd < 4; ++hd) {
+        float mx = logit[hd][0];
+        for (int p = 1; p < DF; ++p) mx = logit[hd][p] > mx ? logit[hd][p] : mx;
+        float ex[DF], sum = 0.0f;
+        for (int p = 0; p < DF; ++p) { ex[p] = c_exp(logit[hd][p] - mx); sum = sum + ex[p]; }
+        for (int p = 0; p < DF; ++p) wgt[hd][p] = ex[p] / sum;
+      }
+      tile_zero(wa);
+      for (int p = 0; p < DF; ++p) {
+        Tile vv;
+        tile_load_perm(vv, a.v_buf + (base + (int64_t)tc * DF + p) * 128);
+#pragma unroll
+        for (int M = 0; M < 4; ++M)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) wa.m[M][r] = __builtin_fmaf(wgt[M][p], vv.m[M][r], wa.m[M][r]);
+      }
+    }
+    {  // gating: sigmoid(LN_q(r) Wg + bg)
+      Tile q;
+      tile_load_perm(q, rrow);
+      tile_layer_norm(q, W.qn_s, W.qn_o);
+      Tile gt;
+      tile_zero(gt);
+      tile_gemm(gt, q, W.wg);
+      tile_add_vec(gt, W.gb);
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) wa.m[M][r] = wa.m[M][r] * c_sigmoid(gt.m[M][r]);
+    }
+    {  // output projection + residual
+      Tile o;
+      tile_zero(o);
+      tile_gemm(o, wa, W.wo);
+      tile_add_vec(o, W.ob);
+      Tile r;
+      tile_load_perm(r, rrow);
+      tile_add(r, o);
+      if (valid) tile_store_perm(r, rrow);
+      // resampled transition: r += T(LN(r))
+      Tile x = r;
+      tile_layer_norm(x, W.rt_ln_s, W.rt_ln_o);
+      Tile acc;
+      tile_zero(acc);
+      for (int ck = 0; ck < 2; ++ck) {
+        Tile hid;
+        tile_zero(hid);
+        tile_gemm(hid, x, W.rt_w1 + ck * 64 * 64);
+        tile_add_vec(hid, W.rt_b1 + ck * 128);
+        tile_relu(hid);
+        tile_gemm(acc, hid, W.rt_w2 + ck * 64 * 64);
+      }
+      tile_add_vec(acc, W.rt_b2);
+      tile_load_perm(r, rrow);
+      tile_add(r, acc);
+      if (valid) tile_store_perm(r, rrow);
+    }
+    if (blk < 2) {  // original transition (block 3's is dead: only "resampled" is returned)
+      for (int p = 0; p < DF; ++p) {
+        float* orow = a.o_buf + (base + (int64_t)tc * DF + p) * 128;
+        Tile x;
+        tile_load_perm(x, orow);
+        tile_layer_norm(x, W.ot_ln_s, W.ot_ln_o);
+        Tile acc;
+        tile_zero(acc);
+        for (int ck = 0; ck < 2; ++ck) {
+          Tile hid;
+          tile_zero(hid);
+          tile_gemm(hid, x, W.ot_w1 + ck * 64 * 64);
+          tile_add_vec(hid, W.ot_b1 + ck * 128);
+          tile_relu(hid);
+          tile_gemm(acc, hid, W.ot_w2 + ck * 64 * 64);
+        }
+        tile_add_vec(acc, W.ot_b2);
+        tile_load_perm(x, orow);
+        tile_add(x, acc);
+        if (valid) tile_store_perm(x, orow);
+      }
+    }
+  }
+  // ---- spherical norm, down_proj, FSQ
+  Tile r;
+  tile_load_perm(r, rrow);
+  float s = 0.0f;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s = s + r.m[M][q] * r.m[M][q];
+  float nrm = sqrtf(s + __shfl_xor(s, 32, 64)) + 1e-6f;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) r.m[M][q] = r.m[M][q] / nrm;
+  f32x16 z;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) z[q] = 0.0f;
+  tile_gemm_narrow(z, r, a.down_w);
+  // output o = (q&3) + 8*(q>>2) + 4*half: d<4 in half 0 regs 0..3, d = 4..7 in half 1 regs 0..3
+  uint32_t part_idx = 0;
+  const int h = lane >> 5;
+  const int64_t orow_i = base + t;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int d = q + 4 * h;
+    if (d < a.D) {
+      float zz = z[q] + a.down_b[d];
+      float bnd = c_tanh(zz + a.fsq_shift[d]) * a.fsq_half[d] - a.fsq_off[d];
+      float qv = rintf(bnd);
+      part_idx += (uint32_t)((int)qv + a.fsq_L[d] / 2) * (uint32_t)a.fsq_basis[d];
+      if (valid) {
+        a.bounded_out[orow_i * 8 + d] = bnd;
+        a.quant_out[orow_i * 8 + d] = qv;
+      }
+    }
+  }
+  uint32_t idx = part_idx + (uint32_t)__shfl_xor((int)part_idx, 32, 64);
+  if (valid) {
+    if (h == 0) a.tokens_out[orow_i] = idx;
+    // continuous_embedding_pre_proj in natural channel order
+    float4* pp = reinterpret_cast<float4*>(a.pre_proj_out + orow_i * 128);
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        pp[(32 * M + 8 * q + 4 * h) / 4] = make_float4(r.m[M][4 * q], r.m[M][4 * q + 1], r.m[M][4 * q + 2], r.m[M][4 * q + 3]);
+  }
+}
+
+// ---------------------------------------------------------------------------- tables
+// Y[row] = X[row] · W (+ b); rows of X and Y in perm order, 32 rows per wave.
+__global__ __launch_bounds__(256) void k_table_gemm(const float* __restrict__ X, int n_rows,
+                                                    const float4* __restrict__ Wf, const float* __restrict__ b,
+                                                    float* __restrict__ Y, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int wtile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int row = wtile * 32 + (lane & 31);
+  if (wtile * 32 >= n_rows) return;
+  int rc = row < n_rows ? row : n_rows - 1;
+  Tile x, acc;
+  tile_load_perm(x, X + (int64_t)rc * 128);
+  tile_zero(acc);
+  tile_gemm(acc, x, Wf);
+  if (b) tile_add_vec(acc, b);
+  if (row < n_rows) tile_store_perm(acc, Y + (int64_t)row * ldy);
+}
+
+// --------------------------------------------------------------------------- launchers
+void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st) {
+  hipLaunchKernelGGL(k_prep, dim3(n_prot), dim3(512), 0, st, a);
+}
+void launch_knn(const KnnArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_knn, dim3((unsigned)((a.n_slots + 3) / 4)), dim3(256), 0, st, a);
+}
+void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st) {
+  dim3 grid((unsigned)((a.n_tasks + 3) / 4));
+  if (layer == 0) hipLaunchKernelGGL(k_mpnn<0>, grid, dim3(256), 0, st, a);
+  else if (layer == 1) hipLaunchKernelGGL(k_mpnn<1>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(k_mpnn<2>, grid, dim3(256), 0, st, a);
+}
+void launch_down(int df, const DownArgs& a, hipStream_t st) {
+  dim3 grid((unsigned)((a.n_tiles + 3) / 4));
+  if (df == 1) hipLaunchKernelGGL(k_down<1>, grid, dim3(256), 0, st, a);
+  else if (df == 2) hipLaunchKernelGGL(k_down<2>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(k_down<4>, grid, dim3(256), 0, st, a);
+}
+void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, float* Y, int ldy,
+                       hipStream_t st) {
+  int tiles = (n_rows + 31) / 32;
+  hipLaunchKernelGGL(k_table_gemm, dim3((tiles + 3) / 4), dim3(256), 0, st, X, n_rows, Wf, b, Y, ldy);
+}
+
+}  // namespace pst

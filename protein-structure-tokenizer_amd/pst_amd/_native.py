@@ -1,0 +1,184 @@
+"""ctypes binding of libpst.so (the C ABI in include/pst.h).
+
+The library is built in-tree (`protein-structure-tokenizer_amd/pst_amd/_lib/libpst.so`,
+`make -C protein-structure-tokenizer_amd/csrc`). There is no CPU fallback: if the library or a
+HIP device is missing, loading raises.
+"""
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import params as _params
+from .config import LEVELS
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PST_LIB", os.path.join(_HERE, "_lib", "libpst.so"))
+
+PST_OK, PST_E_INVALID, PST_E_TOO_LARGE, PST_E_TOO_SMALL, PST_E_HIP, PST_E_NOMEM = 0, -1, -2, -3, -4, -5
+ABI_VERSION = 1
+
+
+class PstError(RuntimeError):
+    pass
+
+
+class _ModelDesc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("codebook_size", ctypes.c_int32),
+                ("downsampling_ratio", ctypes.c_int32), ("n_levels", ctypes.c_int32),
+                ("levels", ctypes.c_int32 * 8), ("seq_max_size", ctypes.c_int32),
+                ("graph_max_neighbor", ctypes.c_int32)]
+
+
+_lib = None
+EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "pst_create_error",
+           "pst_tokenize", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
+           "pst_stream", "pst_debug_fetch")
+
+
+def lib():
+    """Load libpst.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PstError(f"libpst.so not found at {LIB_PATH}: build it with "
+                           "`make -C protein-structure-tokenizer_amd/csrc` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.pst_param_count.restype = ctypes.c_size_t
+        L.pst_param_count.argtypes = [ctypes.c_int32]
+        L.pst_create.argtypes = [ctypes.c_int32, ctypes.POINTER(_ModelDesc), P, ctypes.c_size_t, ctypes.POINTER(P)]
+        L.pst_destroy.argtypes = [P]
+        L.pst_last_error.restype = ctypes.c_char_p
+        L.pst_last_error.argtypes = [P]
+        L.pst_create_error.restype = ctypes.c_char_p
+        L.pst_tokenize.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
+        L.pst_tokenize_device.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
+        L.pst_aux.argtypes = [P, P, P, P]
+        L.pst_codebook_aux.argtypes = [P, P, P, P]
+        L.pst_sync.argtypes = [P]
+        L.pst_stream.restype = P
+        L.pst_stream.argtypes = [P]
+        L.pst_debug_fetch.argtypes = [P, ctypes.c_int32, P, ctypes.c_size_t]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def raise_for(code: int, msg: str):
+    """Map C ABI codes onto the reference's exception types (inference_runner.py:52-62)."""
+    if code == PST_OK:
+        return
+    if code in (PST_E_TOO_LARGE, PST_E_TOO_SMALL):
+        raise NotImplementedError(msg)
+    if code == PST_E_INVALID:
+        raise ValueError(msg)
+    raise PstError(f"libpst error {code}: {msg}")
+
+
+def pack_samples(samples) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """List of ProteinStructureSample → (positions f64 [R,37,3], flags u8 [R,37], offsets i64 [B+1])."""
+    n = [s.nb_residues for s in samples]
+    off = np.zeros(len(samples) + 1, np.int64)
+    off[1:] = np.cumsum(n)
+    pos = np.ascontiguousarray(np.concatenate([s.atom37_positions for s in samples]), dtype=np.float64)
+    flags = np.ascontiguousarray(np.concatenate([s.atom_flags() for s in samples]), dtype=np.uint8)
+    return pos, flags, off
+
+
+class Tokenizer:
+    """One libpst context (one GPU): encoder-half weights resident in HBM."""
+
+    def __init__(self, device: int = 0, codebook_size: int = 4096, downsampling_ratio: int = 1,
+                 params_blob: Optional[np.ndarray] = None, levels: Optional[Sequence[int]] = None):
+        L = lib()
+        self.levels = tuple(levels or LEVELS[codebook_size])
+        self.D = len(self.levels)
+        self.df = downsampling_ratio
+        self.codebook_size = int(np.prod(self.levels))
+        if params_blob is None:
+            params_blob = _params.random_blob(self.D, 0)
+        self.blob = np.ascontiguousarray(params_blob, dtype=np.float32)
+        n = L.pst_param_count(self.D)
+        if self.blob.size != n:
+            raise ValueError(f"parameter blob has {self.blob.size} floats, expected {n}")
+        desc = _ModelDesc(ABI_VERSION, self.codebook_size, downsampling_ratio, self.D,
+                          (ctypes.c_int32 * 8)(*(list(self.levels) + [0] * (8 - self.D))), 512, 50)
+        h = ctypes.c_void_p()
+        rc = L.pst_create(device, ctypes.byref(desc), _ptr(self.blob), self.blob.size, ctypes.byref(h))
+        if rc != PST_OK:
+            raise_for(rc, L.pst_create_error().decode())
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pst_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != PST_OK:
+            raise_for(rc, lib().pst_last_error(self._h).decode())
+
+    @property
+    def stream(self) -> int:
+        return lib().pst_stream(self._h)
+
+    def tokenize_packed(self, pos, flags, offsets):
+        """Ragged batch → (tokens [R] uint32 in raw-offset layout, n_tokens [B], n_nodes [B])."""
+        pos = np.ascontiguousarray(pos, np.float64)
+        flags = np.ascontiguousarray(flags, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        B = len(offsets) - 1
+        R = int(offsets[-1])
+        tok = np.zeros(max(R, 1), np.uint32)
+        nt = np.zeros(B, np.int32)
+        nn = np.zeros(B, np.int32)
+        self._check(lib().pst_tokenize(self._h, _ptr(pos), _ptr(flags), _ptr(offsets), B, _ptr(tok), _ptr(nt), _ptr(nn)))
+        return tok, nt, nn
+
+    def tokenize(self, samples) -> List[np.ndarray]:
+        pos, flags, off = pack_samples(samples)
+        tok, nt, _ = self.tokenize_packed(pos, flags, off)
+        return [tok[off[b]:off[b] + nt[b]].copy() for b in range(len(samples))]
+
+    def tokenize_device(self, d_pos: int, d_flags: int, offsets: np.ndarray, d_tokens: int, d_ntok: int, d_nnodes: int):
+        """Device pointers (ints, e.g. torch tensor.data_ptr()); asynchronous on self.stream."""
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        self._check(lib().pst_tokenize_device(self._h, ctypes.c_void_p(d_pos), ctypes.c_void_p(d_flags), _ptr(offsets),
+                                              len(offsets) - 1, ctypes.c_void_p(d_tokens), ctypes.c_void_p(d_ntok),
+                                              ctypes.c_void_p(d_nnodes)))
+
+    def sync(self):
+        self._check(lib().pst_sync(self._h))
+
+    def aux(self, R: int):
+        b = np.zeros((R, self.D), np.float32)
+        q = np.zeros((R, self.D), np.float32)
+        pp = np.zeros((R, 128), np.float32)
+        self._check(lib().pst_aux(self._h, _ptr(b), _ptr(q), _ptr(pp)))
+        return dict(bounded=b, quantize=q, pre_proj=pp)
+
+    def debug_fetch(self, which: int, R: int):
+        if which in (1, 2, 3):
+            out = np.zeros((R, 128), np.float32)
+        elif which == 10:
+            out = np.zeros((R * 50, 32), np.float32)
+        elif which == 11:
+            out = np.zeros(R * 50, np.int32)
+        elif which == 12:
+            out = np.zeros(R, np.int32)
+        else:
+            raise ValueError(which)
+        self._check(lib().pst_debug_fetch(self._h, which, _ptr(out), out.nbytes))
+        return out

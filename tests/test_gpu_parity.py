@@ -1,0 +1,125 @@
+"""GPU parity: libpst (HIP, through the C ABI) against the CPU oracle, bit for bit.
+
+The canonical numerics make the GPU path and the oracle compute the same
+IEEE operation sequence, so every float output is compared BITWISE and token ids exactly.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pst_amd import params as P
+from pst_amd import synthetic
+from pst_amd.config import LEVELS
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+_TOK = {}
+
+
+def tokenizer(cb=4096, df=1, seed=1234):
+    key = (cb, df, seed)
+    if key not in _TOK:
+        os.environ["PST_DEBUG"] = "1"
+        from pst_amd._native import Tokenizer
+        _TOK[key] = Tokenizer(0, cb, df, P.random_blob(len(LEVELS[cb]), seed))
+    return _TOK[key]
+
+
+def _samples_from(npz, case):
+    from pst_amd.sample import ProteinStructureSample
+    pos = npz[case + "/in_positions"].astype(np.float64)
+    fl = npz[case + "/in_flags"]
+    n = pos.shape[0]
+    return ProteinStructureSample(None, n, np.zeros((n, 21)), pos, (fl & 1).astype(bool),
+                                  ((fl >> 1) & 1).astype(bool), 0.0, 1)
+
+
+def _check_batch(samples, cb, df, seed=1234, layers=True):
+    tk = tokenizer(cb, df, seed)
+    from pst_amd._native import pack_samples
+    pos, flags, off = pack_samples(samples)
+    tok, nt, nn = tk.tokenize_packed(pos, flags, off)
+    R = int(off[-1])
+    aux = tk.aux(R)
+    feat = tk.debug_fetch(10, R)
+    snd = tk.debug_fetch(11, R)
+    hl = [tk.debug_fetch(w, R) for w in (1, 2, 3)] if layers else None
+    blob = P.random_blob(len(LEVELS[cb]), seed)
+    for b, s in enumerate(samples):
+        o = O.tokenize(blob, LEVELS[cb], df, s.atom37_positions, s.atom_flags(), want_layers=layers)
+        g = o["graph"]
+        n = g["n"]
+        assert nn[b] == n
+        assert nt[b] == n // df
+        base = off[b]
+        # graph: senders and features bitwise
+        gs = snd[base * 50: (base + n) * 50]
+        valid = g["senders"] >= 0
+        assert np.array_equal(gs[valid] - base, g["senders"][valid])
+        gf = feat[base * 50: (base + n) * 50]
+        assert np.array_equal(gf.view(np.uint32), g["feat"].view(np.uint32)), "edge features differ"
+        if layers:
+            for li in range(3):
+                got = hl[li][base: base + n]
+                want = o["h_layers"][li + 1]
+                assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"node features differ after layer {li + 1}: max {np.abs(got - want).max()}"
+        T = n // df
+        assert np.array_equal(tok[base: base + T], o["tokens"])
+        assert np.array_equal(aux["bounded"][base: base + T].view(np.uint32), o["b"].view(np.uint32))
+        assert np.array_equal(aux["pre_proj"][base: base + T].view(np.uint32), o["pre_proj"].view(np.uint32))
+
+
+def test_single_protein_df1():
+    _check_batch([synthetic.synthetic_protein(64, 9)], 4096, 1)
+
+
+def test_ragged_batch_df1():
+    F = np.load(os.path.join(GOLD, "forward_golden_f64.npz"))
+    samples = [synthetic.synthetic_protein(n, 100 + n) for n in (50, 51, 77, 130, 257)]
+    samples.append(_samples_from(F, "syn96_missing_k4096_df1"))
+    _check_batch(samples, 4096, 1)
+
+
+def test_short_protein_branch():
+    G = np.load(os.path.join(GOLD, "graph_golden.npz"))
+    _check_batch([_samples_from(G, "syn56_missing9_df1"), synthetic.synthetic_protein(50, 3)], 4096, 1)
+
+
+@pytest.mark.parametrize("cb,df", [(64000, 4), (4096, 2), (432, 1), (1728, 1)])
+def test_other_models(cb, df):
+    _check_batch([synthetic.synthetic_protein(n, 7 + n) for n in (60, 130, 203)], cb, df, layers=False)
+
+
+def test_tokens_match_reference_golden():
+    """End to end vs the REFERENCE forward (float64 under the shim): identical ids."""
+    F = np.load(os.path.join(GOLD, "forward_golden_f64.npz"))
+    for case in sorted({k.split("/")[0] for k in F.files}):
+        n, T, cb, df, D, seed = (int(v) for v in F[case + "/meta"])
+        tk = tokenizer(cb, df, seed)
+        toks = tk.tokenize([_samples_from(F, case)])[0]
+        assert np.array_equal(toks, F[case + "/tokens"]), case
+
+
+def test_casp14_batch():
+    C = np.load(os.path.join(GOLD, "casp14_atom37.npz"))
+    from pst_amd.sample import ProteinStructureSample
+    off = C["offsets"]
+    samples = []
+    for b in range(0, len(off) - 1, 5):  # every 5th protein keeps the CPU oracle fast
+        pos = C["positions"][off[b]:off[b + 1]].astype(np.float64)
+        fl = C["flags"][off[b]:off[b + 1]]
+        n = pos.shape[0]
+        samples.append(ProteinStructureSample(None, n, np.zeros((n, 21)), pos, (fl & 1).astype(bool),
+                                              ((fl >> 1) & 1).astype(bool), 0.0, 1))
+    _check_batch(samples, 4096, 1, layers=False)
+
+
+def test_size_gates_raise_like_reference():
+    tk = tokenizer()
+    with pytest.raises(NotImplementedError):
+        tk.tokenize([synthetic.synthetic_protein(513, 1)])
+    with pytest.raises(NotImplementedError):
+        tk.tokenize([synthetic.synthetic_protein(49, 1)])
