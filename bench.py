@@ -1,0 +1,173 @@
+"""Benchmark: residues tokenized/s (codebook 4096, df 1) on MI355X — BASELINE.json's metric.
+
+One step = one pass of the tokenize hot path (graph build → 3 fused MPNN layers →
+downsampler → FSQ ids) over one batch of 1024 synthetic proteins x 256 residues per GPU, with
+the atom37 inputs already resident in HBM (pst_tokenize_device). Multi-GPU: one process per
+GPU (torchrun), independent proteins per rank, no collective on the data path ("scaling":
+"weak": every rank runs the full 1024 x 256 workload on its own proteins). Prints ONE JSON line
+on rank 0.
+
+Also reported: the dominant kernel's roofline (HIP events on the library's stream), the CPU
+baseline (the oracle, C, on a bounded sample on this host's cores) and the GPU-vs-oracle token
+exact-match rate on that sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "protein-structure-tokenizer_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from pst_amd import params as P  # noqa: E402
+from pst_amd import synthetic  # noqa: E402
+from pst_amd._native import Tokenizer, pack_samples  # noqa: E402
+
+N_PROT, N_RES, CODEBOOK, DF = 1024, 256, 4096, 1
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA / VALU dense peak
+PEAK_HBM_GBS = 8000.0
+H, K = 128, 50
+# Algorithmic FLOPs (padding and dead code removed) of the dominant kernel
+# k_mpnn<1> = edge MLP of layer 1 + message MLP of layer 2 over 50 edges, + layer-2 node FFN:
+MLP_FLOP = 2 * (3 * H * H + H * H + H * H)          # 163 840 per edge per 384-128-128-128 MLP
+MPNN1_ALG_FLOP_PER_RES = K * 2 * MLP_FLOP + 2 * (H * 4 * H + 4 * H * H)   # 16 646 144
+PATH_ALG_FLOP_PER_RES = 44_715_008                  # SURVEY §8d, whole path at df = 1
+# What k_mpnn<1> executes (node-projection split of the 384-wide first layers)
+MPNN1_EXEC_FLOP_PER_RES = K * 6 * 2 * H * H + 4 * 2 * H * H + 2 * (H * 4 * H + 4 * H * H)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--proteins", type=int, default=N_PROT)
+    ap.add_argument("--residues", type=int, default=N_RES)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=128, help="proteins in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    # synthetic workload of this rank (different proteins per rank)
+    samples = synthetic.synthetic_batch(args.proteins, args.residues, seed=1000 + rank * 100_000)
+    pos, flags, off = pack_samples(samples)
+    d_pos = torch.from_numpy(pos).to(dev)
+    d_flags = torch.from_numpy(flags).to(dev)
+    R = int(off[-1])
+    d_tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    d_ntok = torch.zeros(len(samples), dtype=torch.int32, device=dev)
+    d_nn = torch.zeros(len(samples), dtype=torch.int32, device=dev)
+    blob = P.random_blob(6, 1234)
+    tk = Tokenizer(local, CODEBOOK, DF, blob)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        tk.tokenize_device(d_pos.data_ptr(), d_flags.data_ptr(), off, d_tok.data_ptr(), d_ntok.data_ptr(),
+                           d_nn.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    tk.sync()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    tk.sync()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    residues_per_rank = R
+    value = world * residues_per_rank * args.steps / elapsed
+
+    # per-stage device times (HIP events on the library stream), averaged over 3 extra steps
+    tk.set_timing(True)
+    stage = None
+    for _ in range(3):
+        step()
+        st = tk.stage_ms()
+        stage = st if stage is None else {k: stage[k] + st[k] for k in st}
+    stage = {k: v / 3 for k, v in stage.items()}
+    tk.set_timing(False)
+    dom_ms = stage["mpnn1"]
+    achieved = MPNN1_ALG_FLOP_PER_RES * residues_per_rank / (dom_ms * 1e-3) / 1e12
+    roofline = {
+        "kernel": "k_mpnn<1> (edge MLP L1 + message MLP L2 + node FFN, fused)",
+        "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+        "launch_ms": round(dom_ms, 3),
+        "executed_tflops": round(MPNN1_EXEC_FLOP_PER_RES * residues_per_rank / (dom_ms * 1e-3) / 1e12, 2),
+        "stage_ms": {k: round(v, 3) for k, v in stage.items()},
+        "path_alg_tflops": round(PATH_ALG_FLOP_PER_RES * residues_per_rank / (sum(stage.values()) * 1e-3) / 1e12, 2),
+    }
+
+    cpu = None
+    exact = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        n = min(args.cpu_sample, len(samples))
+        sub_off = off[:n + 1]
+        sub_R = int(sub_off[-1])
+        t1 = time.perf_counter()
+        otok, ont = O.tokenize_batch(blob, (4,) * 6, DF, pos[:sub_R], flags[:sub_R], sub_off, n_threads=args.cpu_threads)
+        cpu_s = time.perf_counter() - t1
+        cpu = {"value": round(sub_R / cpu_s, 1), "unit": "residues/s", "cores": args.cpu_threads, "kind": "port",
+               "sample": f"first {n} of the synthetic proteins ({sub_R} residues), oracle/pst_oracle.c, "
+                         f"OpenMP over proteins, {cpu_s:.1f} s"}
+        gtok = d_tok.cpu().numpy().view(np.uint32)
+        match = int(np.sum(gtok[:sub_R] == otok[:sub_R]))
+        exact = {"tokens_compared": sub_R, "identical": match, "rate": match / sub_R, "against": "oracle (bitwise canonical path)"}
+
+    if rank == 0:
+        out = {
+            "metric": "residues tokenized/sec (cb=4096, df=1)",
+            "value": round(value, 1),
+            "unit": "residues/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (random-walk backbones, random-init weights of the reference architecture)",
+            "config": {"workload": f"{args.proteins} proteins x {args.residues} residues per GPU, codebook 4096, df 1",
+                       "codebook_size": CODEBOOK, "df": DF, "proteins_per_gpu": args.proteins,
+                       "residues_per_protein": args.residues, "parallelism": f"dp{world} (independent proteins)"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "exact_match": exact,
+        }
+        print(json.dumps(out), flush=True)
+    tk.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

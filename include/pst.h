@@ -129,6 +129,12 @@ int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t
 
 int pst_sync(pst_ctx* ctx);
 
+/* Per-stage timing of the last tokenize call (HIP events on the context's stream):
+ * ms[0..5] = prep, knn, mpnn layer 0, mpnn layer 1, mpnn layer 2, downsampler+FSQ. */
+#define PST_N_STAGES 6
+int pst_set_timing(pst_ctx* ctx, int32_t enable);
+int pst_get_timing(pst_ctx* ctx, float* ms);
+
 /* Stream the context launches on (hipStream_t), for event timing by callers. */
 void* pst_stream(pst_ctx* ctx);
 

@@ -214,10 +214,17 @@ struct pst_ctx {
   } w{};
   std::vector<int64_t> h_offsets;
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
+  // optional per-stage timing (HIP events on ctx->stream)
+  bool timing = false;
+  hipEvent_t ev[PST_N_STAGES + 1] = {};
   int64_t dbg_cap = 0;
 };
 
 namespace {
+
+inline void mark(pst_ctx* ctx, int i) {
+  if (ctx->timing) (void)hipEventRecord(ctx->ev[i], ctx->stream);
+}
 
 #define HIPCHK(x)                                                                   \
   do {                                                                              \
@@ -448,10 +455,13 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   HIPCHK(hipMemsetAsync(w.node_local, 0xff, sizeof(int32_t) * Rpad, st));
   HIPCHK(hipMemsetAsync(w.node_prot, 0, sizeof(int32_t) * Rpad, st));
 
+  mark(ctx, 0);
   pst::PrepArgs pa{d_pos, d_flags, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca};
   pst::launch_prep(pa, n_prot, st);
+  mark(ctx, 1);
   pst::KnnArgs ka{Rpad, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, w.senders, w.deg, w.feat};
   pst::launch_knn(ka, st);
+  mark(ctx, 2);
 
   const float* A = ctx->d_arena;
   auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(A + o); };
@@ -496,6 +506,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.h_out = hbuf[l + 1];
     m.P_out = pbuf[l];
     pst::launch_mpnn(l, m, st);
+    mark(ctx, 3 + l);
     if (ctx->dbg[l]) HIPCHK(hipMemcpyAsync(ctx->dbg[l], m.h_out, sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
   }
   // downsampler's original track works on a copy of h3 (h3 stays available to pst_debug_fetch)
@@ -536,6 +547,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   d.quant_out = w.quant;
   d.pre_proj_out = w.pre_proj;
   if (d.n_tiles > 0) pst::launch_down(ctx->df, d, st);
+  mark(ctx, 6);
   HIPCHK(hipGetLastError());
   ctx->last_R = R;
   ctx->last_Rpad = Rpad;
@@ -552,6 +564,22 @@ __global__ void k_ntok(const int32_t* n_nodes, int32_t* n_tok, int B, int df) {
 }  // namespace
 
 extern "C" {
+
+int pst_set_timing(pst_ctx* ctx, int32_t enable) {
+  if (!ctx) return PST_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (enable && !ctx->ev[0])
+    for (int i = 0; i <= PST_N_STAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
+  ctx->timing = enable != 0;
+  return PST_OK;
+}
+
+int pst_get_timing(pst_ctx* ctx, float* ms) {
+  if (!ctx || !ctx->timing || !ms) return PST_E_INVALID;
+  HIPCHK(hipEventSynchronize(ctx->ev[PST_N_STAGES]));
+  for (int i = 0; i < PST_N_STAGES; ++i) HIPCHK(hipEventElapsedTime(&ms[i], ctx->ev[i], ctx->ev[i + 1]));
+  return PST_OK;
+}
 
 size_t pst_param_count(int32_t n_levels) {
   HostParams P;
@@ -620,6 +648,8 @@ int pst_destroy(pst_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (int l = 0; l < 3; ++l)
     if (ctx->dbg[l]) (void)hipFree(ctx->dbg[l]);
+  for (int i = 0; i <= PST_N_STAGES; ++i)
+    if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
   for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

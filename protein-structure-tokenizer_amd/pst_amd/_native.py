@@ -34,7 +34,8 @@ class _ModelDesc(ctypes.Structure):
 _lib = None
 EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "pst_create_error",
            "pst_tokenize", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
-           "pst_stream", "pst_debug_fetch")
+           "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing")
+STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
 def lib():
@@ -61,6 +62,8 @@ def lib():
         L.pst_stream.restype = P
         L.pst_stream.argtypes = [P]
         L.pst_debug_fetch.argtypes = [P, ctypes.c_int32, P, ctypes.c_size_t]
+        L.pst_set_timing.argtypes = [P, ctypes.c_int32]
+        L.pst_get_timing.argtypes = [P, P]
         _lib = L
     return _lib
 
@@ -158,6 +161,15 @@ class Tokenizer:
         self._check(lib().pst_tokenize_device(self._h, ctypes.c_void_p(d_pos), ctypes.c_void_p(d_flags), _ptr(offsets),
                                               len(offsets) - 1, ctypes.c_void_p(d_tokens), ctypes.c_void_p(d_ntok),
                                               ctypes.c_void_p(d_nnodes)))
+
+    def set_timing(self, on: bool = True):
+        self._check(lib().pst_set_timing(self._h, 1 if on else 0))
+
+    def stage_ms(self):
+        """Per-stage device time (ms) of the last call, from HIP events on self.stream."""
+        ms = np.zeros(len(STAGES), np.float32)
+        self._check(lib().pst_get_timing(self._h, _ptr(ms)))
+        return dict(zip(STAGES, ms.tolist()))
 
     def sync(self):
         self._check(lib().pst_sync(self._h))
