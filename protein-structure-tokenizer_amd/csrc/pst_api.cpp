@@ -206,7 +206,7 @@ struct pst_ctx {
     int64_t* offsets;
     int32_t *n_nodes, *node_local, *node_prot, *senders, *deg, *tile_prot, *tile_t0;
     double *frame, *cen, *ca;
-    float *feat, *e0, *e1, *h0, *h1, *P0, *P1, *r_buf, *v_buf, *bounded, *quant, *pre_proj;
+    float *feat, *e0, *e1, *h0, *h1, *P0, *P1, *agg, *r_buf, *v_buf, *bounded, *quant, *pre_proj;
     double* pos;
     uint8_t* flags;
     uint32_t* tokens;
@@ -380,7 +380,7 @@ int ensure_workspace(pst_ctx* ctx, int64_t R, int B) {
       {(void**)&w.frame, sizeof(double) * 9 * Rpad},    {(void**)&w.cen, sizeof(double) * 3 * Rpad},
       {(void**)&w.ca, sizeof(double) * 3 * Rpad},       {(void**)&w.feat, sizeof(float) * 32 * E},
       {(void**)&w.e0, sizeof(float) * 128 * E},         {(void**)&w.e1, sizeof(float) * 128 * E},
-      {(void**)&w.h0, sizeof(float) * 128 * Rpad},      {(void**)&w.h1, sizeof(float) * 128 * Rpad},
+      {(void**)&w.h0, sizeof(float) * 128 * Rpad},      {(void**)&w.agg, sizeof(float) * 128 * Rpad},      {(void**)&w.h1, sizeof(float) * 128 * Rpad},
       {(void**)&w.P0, sizeof(float) * 512 * Rpad},      {(void**)&w.P1, sizeof(float) * 512 * Rpad},
       {(void**)&w.r_buf, sizeof(float) * 128 * Rpad},   {(void**)&w.v_buf, sizeof(float) * 128 * Rpad},
       {(void**)&w.bounded, sizeof(float) * 8 * Rpad},   {(void**)&w.quant, sizeof(float) * 8 * Rpad},
@@ -477,6 +477,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.senders = w.senders;
     m.deg = w.deg;
     m.node_local = w.node_local;
+    m.agg = w.agg;
     m.feat = w.feat;
     m.Ttab = ctx->d_T;
     m.W_embed = F4(ctx->emb_w);

@@ -18,6 +18,22 @@ namespace pst {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------ canonical f32 math
+// p / q for tanh's operand range (q in [4.9e-3, 1], |p| <= 1, no denormals): the Newton /
+// Markstein core of the IEEE f32 division sequence without its range scaling and special-case
+// fixup (v_div_scale / v_div_fixup are no-ops here). Correctly rounded, so bit-identical to
+// p / q on any IEEE machine; tools/micro/div_check.hip verifies c_tanh against the IEEE-division
+// form for all 2^32 float32 inputs.
+__device__ __forceinline__ float div_tanh(float p, float q) {
+  float r = __builtin_amdgcn_rcpf(q);
+  float e = __builtin_fmaf(-q, r, 1.0f);
+  r = __builtin_fmaf(e, r, r);
+  float y = p * r;
+  float e2 = __builtin_fmaf(-q, y, p);
+  y = __builtin_fmaf(e2, r, y);
+  float e3 = __builtin_fmaf(-q, y, p);
+  return __builtin_fmaf(e3, r, y);
+}
+
 __device__ __forceinline__ float c_tanh(float a) {
   const float clamp = 7.99881172180175781f;
   float x = fminf(fmaxf(a, -clamp), clamp);
@@ -32,7 +48,7 @@ __device__ __forceinline__ float c_tanh(float a) {
   float q = __builtin_fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
   q = __builtin_fmaf(x2, q, 2.26843463243900e-03f);
   q = __builtin_fmaf(x2, q, 4.89352518554385e-03f);
-  float r = p / q;
+  float r = div_tanh(p, q);
   return fabsf(a) < 0.0004f ? a : r;
 }
 
@@ -40,6 +56,50 @@ __device__ __forceinline__ float c_gelu(float x) {
   float x3 = x * (x * x);
   float inner = 0.797884583473205566f * (x + 0.0447149984538555145f * x3);
   float cdf = 0.5f * (1.0f + c_tanh(inner));
+  return x * cdf;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Two c_gelu evaluations with packed f32 math (v_pk_fma/mul/add_f32): bit-identical to c_gelu
+// on each element, about half the VALU issue cycles.
+__device__ __forceinline__ f32x2 c_gelu2(f32x2 x) {
+  const f32x2 clampv = {7.99881172180175781f, 7.99881172180175781f};
+  f32x2 x2_ = x * x;
+  f32x2 x3 = x * x2_;
+  f32x2 inner = (f32x2){0.797884583473205566f, 0.797884583473205566f} *
+                (x + (f32x2){0.0447149984538555145f, 0.0447149984538555145f} * x3);
+  f32x2 a = inner;
+  f32x2 xc = __builtin_elementwise_min(__builtin_elementwise_max(a, -clampv), clampv);
+  f32x2 s = xc * xc;
+  f32x2 p = pk_fma(s, (f32x2){-2.76076847742355e-16f, -2.76076847742355e-16f},
+                   (f32x2){2.00018790482477e-13f, 2.00018790482477e-13f});
+  p = pk_fma(s, p, (f32x2){-8.60467152213735e-11f, -8.60467152213735e-11f});
+  p = pk_fma(s, p, (f32x2){5.12229709037114e-08f, 5.12229709037114e-08f});
+  p = pk_fma(s, p, (f32x2){1.48572235717979e-05f, 1.48572235717979e-05f});
+  p = pk_fma(s, p, (f32x2){6.37261928875436e-04f, 6.37261928875436e-04f});
+  p = pk_fma(s, p, (f32x2){4.89352455891786e-03f, 4.89352455891786e-03f});
+  p = xc * p;
+  f32x2 q = pk_fma(s, (f32x2){1.19825839466702e-06f, 1.19825839466702e-06f},
+                   (f32x2){1.18534705686654e-04f, 1.18534705686654e-04f});
+  q = pk_fma(s, q, (f32x2){2.26843463243900e-03f, 2.26843463243900e-03f});
+  q = pk_fma(s, q, (f32x2){4.89352518554385e-03f, 4.89352518554385e-03f});
+  // division core (see div_tanh), packed
+  f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+  const f32x2 one = {1.0f, 1.0f};
+  f32x2 e = pk_fma(-q, r, one);
+  r = pk_fma(e, r, r);
+  f32x2 y = p * r;
+  f32x2 e2 = pk_fma(-q, y, p);
+  y = pk_fma(e2, r, y);
+  f32x2 e3 = pk_fma(-q, y, p);
+  y = pk_fma(e3, r, y);
+  f32x2 t;
+  t.x = fabsf(a.x) < 0.0004f ? a.x : y.x;
+  t.y = fabsf(a.y) < 0.0004f ? a.y : y.y;
+  f32x2 cdf = (f32x2){0.5f, 0.5f} * (one + t);
   return x * cdf;
 }
 
@@ -202,23 +262,69 @@ __device__ __forceinline__ void tile_store_blk(const Tile& t, float* __restrict_
 #ifndef GEMM_DEPTH
 #define GEMM_DEPTH 4
 #endif
-__device__ __forceinline__ void tile_gemm(Tile& acc, const Tile& X, const float4* __restrict__ Wf) {
+// Generic form: the B operand of k-step t is f(t, X[t]) — the previous layer's activation
+// (bias + GELU, bias + ReLU, ...) evaluated just in time, one element per k-step, so its VALU
+// work issues in the shadow of the current k-step's four MFMAs instead of as a separate
+// VALU phase between GEMMs. The schedule interleaves MFMA and VALU groups explicitly.
+template <typename F>
+__device__ __forceinline__ void tile_gemm_f(Tile& acc, const Tile& X, const float4* __restrict__ Wf, F&& f) {
   __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
   const int vo = lane_id() * 16;
   float4 ring[GEMM_DEPTH];
 #pragma unroll
   for (int i = 0; i < GEMM_DEPTH; ++i) ring[i] = buf_load4(rs, vo, i * 1024);
+  // activations run one group of 4 k-steps ahead (two packed pairs per group)
+  f32x2 bq[2], bn[2];
 #pragma unroll
-  for (int t = 0; t < 64; ++t) {
-    float4 a = ring[t % GEMM_DEPTH];
-    if (t + GEMM_DEPTH < 64) ring[t % GEMM_DEPTH] = buf_load4(rs, vo, (t + GEMM_DEPTH) * 1024);
-    float b = X.m[t / 16][t % 16];
-    acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b, acc.m[0], 0, 0, 0);
-    acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b, acc.m[1], 0, 0, 0);
-    acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b, acc.m[2], 0, 0, 0);
-    acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b, acc.m[3], 0, 0, 0);
+  for (int j = 0; j < 2; ++j) bq[j] = f(2 * j, (f32x2){X.m[0][2 * j], X.m[0][2 * j + 1]});
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = 4 * g + j;
+      float4 a = ring[t % GEMM_DEPTH];
+      if (t + GEMM_DEPTH < 64) ring[t % GEMM_DEPTH] = buf_load4(rs, vo, (t + GEMM_DEPTH) * 1024);
+      if (g < 15 && (j & 1) == 0) {
+        const int u = t + 4;
+        bn[j >> 1] = f(u, (f32x2){X.m[u / 16][u % 16], X.m[u / 16][u % 16 + 1]});
+      }
+      const float b = (j & 1) ? bq[j >> 1].y : bq[j >> 1].x;
+      acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b, acc.m[0], 0, 0, 0);
+      acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b, acc.m[1], 0, 0, 0);
+      acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b, acc.m[2], 0, 0, 0);
+      acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b, acc.m[3], 0, 0, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);
+    bq[0] = bn[0];
+    bq[1] = bn[1];
   }
+}
+
+// Activation functors: f(t, {x_t, x_t+1}) -> B operands of k-steps t, t+1.
+struct ActId {
+  __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return x; }
+};
+
+// bias (perm-ordered vector, this lane's half) + GELU
+struct ActBiasGelu {
+  const float* b;
+  __device__ __forceinline__ f32x2 operator()(int t, f32x2 x) const {
+    const float* bb = b + (lane_id() >> 5) * 64 + t;
+    return c_gelu2(x + (f32x2){bb[0], bb[1]});
+  }
+};
+
+struct ActBiasRelu {
+  const float* b;
+  __device__ __forceinline__ f32x2 operator()(int t, f32x2 x) const {
+    const float* bb = b + (lane_id() >> 5) * 64 + t;
+    f32x2 v = x + (f32x2){bb[0], bb[1]};
+    return (f32x2){v.x > 0.0f ? v.x : 0.0f, v.y > 0.0f ? v.y : 0.0f};
+  }
+};
+
+__device__ __forceinline__ void tile_gemm(Tile& acc, const Tile& X, const float4* __restrict__ Wf) {
+  tile_gemm_f(acc, X, Wf, ActId{});
 }
 
 // acc(one 32-output accumulator) += X · W, W: [64 k-steps][64 lanes] f32 (K = 128)

@@ -70,6 +70,7 @@ struct MpnnArgs {
   const float4* ff_w2;  // [4 chunks][64][64]
   const float* ff_b2;
   const float4* proj_w;  // [4][64][64]: next kernel's E_s, E_r, M_s, M_r projections (or null)
+  float* agg;  // [n_tasks][32][128] scratch: segment sums (perm order)
   // outputs
   float* e_out;  // blocked (null for the last layer)
   float* h_out;

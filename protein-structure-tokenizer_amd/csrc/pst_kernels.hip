@@ -22,6 +22,9 @@
 
 namespace pst {
 
+#ifndef MPNN_MIN_BLOCKS
+#define MPNN_MIN_BLOCKS 2
+#endif
 #define NATOM 37
 #define KNN 50
 
@@ -257,33 +260,29 @@ __device__ __forceinline__ void tile_add_rows(Tile& acc, const float* __restrict
   tile_add(acc, t);
 }
 
-// 3-layer edge MLP starting from acc = init (already Ps + Pr): acc <- MLP(init, X)
+// 3-layer edge MLP starting from acc = init (already Ps + Pr): acc <- MLP(init, X).
+// Bias + GELU of layers 1 and 2 are applied just in time inside the next GEMM.
 __device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
   tile_gemm(acc, X, W.w0);
-  tile_add_vec(acc, W.b0);
-  tile_gelu(acc);
   Tile a2;
   tile_zero(a2);
-  tile_gemm(a2, acc, W.w1);
-  tile_add_vec(a2, W.b1);
-  tile_gelu(a2);
+  tile_gemm_f(a2, acc, W.w1, ActBiasGelu{W.b0});
   tile_zero(acc);
-  tile_gemm(acc, a2, W.w2);
+  tile_gemm_f(acc, a2, W.w2, ActBiasGelu{W.b1});
   tile_add_vec(acc, W.b2);
 }
 
 template <int LAYER>
-__global__ __launch_bounds__(256, 2) void k_mpnn(MpnnArgs a) {
-  __shared__ float lds_scratch[4][32 * 32];
-  __shared__ float lds_agg[4][32 * 128];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+__global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
+  __shared__ float lds_scratch[4][32 * 36];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (no waterfalls)
   const int64_t task = (int64_t)blockIdx.x * 4 + w;
   if (task >= a.n_tasks) return;
   const int64_t g0 = task * 32;
   float* scratch = lds_scratch[w];
-  float* aggl = lds_agg[w];
+  float* aggl = a.agg + task * 32 * 128;
   const int c = lane & 31, part = lane >> 5;
-  for (int i = lane; i < 32 * 128; i += 64) aggl[i] = 0.0f;
   float carry[4] = {0.f, 0.f, 0.f, 0.f};
 
   for (int blk = 0; blk < 50; ++blk) {
@@ -291,7 +290,11 @@ __global__ __launch_bounds__(256, 2) void k_mpnn(MpnnArgs a) {
     const int rl = te / 50;
     const int64_t g = g0 + rl;
     const int64_t E = g * KNN + (te - 50 * rl);
+#ifdef PST_EXP_HOT_GATHER
+    const int64_t s = g;
+#else
     const int64_t s = a.senders[E];
+#endif
     const int64_t eblk = (task * 50 + blk) * 4096;
     Tile e;
     if (LAYER == 0) {
@@ -340,25 +343,33 @@ __global__ __launch_bounds__(256, 2) void k_mpnn(MpnnArgs a) {
       tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
     }
     mlp3(m, e, a.msg);
-    // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order)
-    const int rA = (32 * blk) / 50;
-    const int lastA = 50 * (rA + 1) - 1 - 32 * blk;  // block-local index of rA's last edge
+    // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order):
+    // transpose through LDS, then each lane runs the sequential chain of its channel; lane
+    // half 0 continues the receiver that owns edge 0 of the block (rA), half 1 starts rA+1.
+    const int rA = (32 * blk) / 50;                    // wave-uniform
+    const int lastA = 50 * (rA + 1) - 1 - 32 * blk;    // block-local index of rA's last edge
+    const int j0 = 32 * blk - 50 * rA;                 // slot of the block's edge 0 within rA
     const int degA = a.deg[g0 + rA];
     const int degB = rA + 1 < 32 ? a.deg[g0 + rA + 1] : 0;
-    const int j0 = 32 * blk - 50 * rA;  // slot of the block's edge 0 in rA
+    const int hiA = min(min(lastA, 31), degA - 1 - j0);  // part 0 sums edges [0, hiA]
+    const int loB = lastA + 1;                           // part 1 sums edges [loB, hiB]
+    const int hiB = min(31, lastA + degB);
 #pragma unroll
     for (int M = 0; M < 4; ++M) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         int ch = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        scratch[ch * 32 + ((lane & 31) ^ ch)] = m.m[M][r];
+        scratch[ch * 36 + (lane & 31)] = m.m[M][r];
       }
       __builtin_amdgcn_wave_barrier();
-      float acc = part == 0 ? carry[M] : 0.0f;
-      for (int ee = 0; ee < 32; ++ee) {
-        bool in = part == 0 ? (ee <= lastA && j0 + ee < degA) : (ee > lastA && ee - lastA - 1 < degB);
-        float v = scratch[c * 32 + (ee ^ c)];
-        if (in) acc = acc + v;
+      const float* srow = scratch + c * 36;
+      float acc;
+      if (part == 0) {
+        acc = carry[M];
+        for (int ee = 0; ee <= hiA; ++ee) acc = acc + srow[ee];
+      } else {
+        acc = 0.0f;
+        for (int ee = loB; ee <= hiB; ++ee) acc = acc + srow[ee];
       }
       __builtin_amdgcn_wave_barrier();
       float other = __shfl_xor(acc, 32, 64);
@@ -370,7 +381,11 @@ __global__ __launch_bounds__(256, 2) void k_mpnn(MpnnArgs a) {
       }
     }
   }
+  // the sums were stored by other lanes of this wave: drain stores, then read back
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   // ---------------- node update for the 32 receivers (lane&31 = receiver)
   const int64_t gl = g0 + (lane & 31);
   Tile x;
@@ -395,9 +410,7 @@ __global__ __launch_bounds__(256, 2) void k_mpnn(MpnnArgs a) {
     Tile hid;
     tile_zero(hid);
     tile_gemm(hid, x, a.ff_w1 + ck * 64 * 64);
-    tile_add_vec(hid, a.ff_b1 + ck * 128);
-    tile_gelu(hid);
-    tile_gemm(out, hid, a.ff_w2 + ck * 64 * 64);
+    tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActBiasGelu{a.ff_b1 + ck * 128});
   }
   tile_add_vec(out, a.ff_b2);
   tile_add(x, out);
@@ -417,7 +430,8 @@ __global__ __launch_bounds__(256, 2) void k_mpnn(MpnnArgs a) {
 // ---------------------------------------------------------------------------- k_down
 template <int DF>
 __global__ __launch_bounds__(256) void k_down(DownArgs a) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile_id = blockIdx.x * 4 + w;
   if (tile_id >= a.n_tiles) return;
   const int b = a.tile_prot[tile_id];
@@ -536,9 +550,7 @@ __global__ __launch_bounds__(256) void k_down(DownArgs a) {
         Tile hid;
         tile_zero(hid);
         tile_gemm(hid, x, W.rt_w1 + ck * 64 * 64);
-        tile_add_vec(hid, W.rt_b1 + ck * 128);
-        tile_relu(hid);
-        tile_gemm(acc, hid, W.rt_w2 + ck * 64 * 64);
+        tile_gemm_f(acc, hid, W.rt_w2 + ck * 64 * 64, ActBiasRelu{W.rt_b1 + ck * 128});
       }
       tile_add_vec(acc, W.rt_b2);
       tile_load_perm(r, rrow);
