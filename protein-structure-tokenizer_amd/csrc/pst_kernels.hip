@@ -295,7 +295,11 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 #else
     const int64_t s = a.senders[E];
 #endif
+#ifdef PST_EXP_HOTE
+    const int64_t eblk = (task * 50) * 4096;
+#else
     const int64_t eblk = (task * 50 + blk) * 4096;
+#endif
     Tile e;
     if (LAYER == 0) {
       // init_edge_embed: chain from T[s-r] over the 27 (+5 zero) features, + bias
@@ -329,9 +333,13 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
       mlp3(acc, ein, a.edge);
       tile_load_blk(e, a.e_in + eblk);
       tile_add(e, acc);
+#ifndef PST_EXP_NOLN
       tile_layer_norm(e, a.edge_ln_s, a.edge_ln_o);
+#endif
     }
+#ifndef PST_EXP_NOSTORE
     if (a.e_out) tile_store_blk(e, a.e_out + eblk);
+#endif
     // message MLP of layer LAYER
     Tile m;
     if (LAYER == 0) {
@@ -354,6 +362,10 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     const int hiA = min(min(lastA, 31), degA - 1 - j0);  // part 0 sums edges [0, hiA]
     const int loB = lastA + 1;                           // part 1 sums edges [loB, hiB]
     const int hiB = min(31, lastA + degB);
+#ifdef PST_EXP_NOAGG
+    if (blk == 49) for (int M = 0; M < 4; ++M) aggl[M] = m.m[M][0] + m.m[M][15];
+    continue;
+#endif
 #pragma unroll
     for (int M = 0; M < 4; ++M) {
 #pragma unroll
