@@ -14,8 +14,11 @@
  *                    Host buffers in, host token ids out (synchronous).
  *   pst_tokenize_device  the same on device-resident buffers, asynchronous on the context's
  *                    stream (what a pipelined runner or bench uses: inputs already in HBM).
- *   pst_aux_device   the non-token QuantizerOutput fields (quantize, continuous_embedding,
+ *   pst_aux          the non-token QuantizerOutput fields (quantize, continuous_embedding,
  *                    continuous_embedding_pre_proj; model/quantize.py:183-242).
+ *   pst_codebook_aux FSQ distances / soft_proba / argmin over the implicit codebook
+ *                    (model/quantize.py:221-239).
+ *   pst_device_count jax.local_device_count (scripts/inference_runner.py:169-177).
  *   pst_sync / pst_last_error / pst_destroy   runtime plumbing (block_until_ready, errors).
  *
  * Errors: every call returns PST_OK (0) or a negative PST_E* code; pst_last_error(ctx) gives
@@ -85,6 +88,10 @@ int pst_destroy(pst_ctx* ctx);
 const char* pst_last_error(const pst_ctx* ctx);
 /* Last error of a failed pst_create (no context exists yet). */
 const char* pst_create_error(void);
+
+/* Number of visible HIP devices (0 when none); replaces jax.local_device_count(backend="gpu")
+ * in InferenceRunner.prepare_devices (scripts/inference_runner.py:169-177). */
+int pst_device_count(int32_t* n);
 
 /*
  * Tokenize a ragged batch of B proteins (host buffers, synchronous).

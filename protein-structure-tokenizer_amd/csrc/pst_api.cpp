@@ -589,6 +589,14 @@ size_t pst_param_count(int32_t n_levels) {
 
 const char* pst_create_error(void) { return g_create_error.c_str(); }
 
+int pst_device_count(int32_t* n) {
+  if (!n) return PST_E_INVALID;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return PST_OK;
+}
+
 int pst_create(int32_t device, const pst_model_desc* desc, const float* params, size_t n_params, pst_ctx** out) {
   g_create_error.clear();
   if (!desc || !params || !out) {

@@ -34,7 +34,7 @@ class _ModelDesc(ctypes.Structure):
 _lib = None
 EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "pst_create_error",
            "pst_tokenize", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
-           "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing")
+           "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing", "pst_device_count")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -64,8 +64,16 @@ def lib():
         L.pst_debug_fetch.argtypes = [P, ctypes.c_int32, P, ctypes.c_size_t]
         L.pst_set_timing.argtypes = [P, ctypes.c_int32]
         L.pst_get_timing.argtypes = [P, P]
+        L.pst_device_count.argtypes = [P]
         _lib = L
     return _lib
+
+
+def device_count() -> int:
+    """Visible HIP devices (pst_device_count)."""
+    n = ctypes.c_int32(0)
+    lib().pst_device_count(ctypes.byref(n))
+    return int(n.value)
 
 
 def _ptr(a: Optional[np.ndarray]):

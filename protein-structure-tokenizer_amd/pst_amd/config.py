@@ -55,6 +55,25 @@ class TokenizerConfig:
         return self.seq_max_size // self.downsampling_ratio
 
 
+def config_from_hydra(cfg) -> TokenizerConfig:
+    """The composed `vq3d_inference` config (`load_config`, as `scripts/tokenize_pdb.py:41-46`
+    builds it) → TokenizerConfig. Reads cfg.model.model.codebook.levels,
+    cfg.model.weight_paths and cfg.data.data.*; rejects settings the device path does not
+    implement (continuous / non-FSQ models)."""
+    m = cfg["model"]
+    d = cfg["data"]["data"]
+    cb = m["model"]["codebook"]
+    if not cb.get("use_codebook", True) or cb.get("method", "fsq") != "fsq":
+        raise NotImplementedError("only FSQ codebook models are tokenized by libpst")
+    levels = tuple(int(x) for x in cb["levels"])
+    return TokenizerConfig(
+        codebook_size=int(cb.get("num_codes", 0)) or int(__import__("math").prod(levels)),
+        downsampling_ratio=int(d["downsampling_ratio"]), levels=levels,
+        seq_max_size=int(d["seq_max_size"]), graph_max_neighbor=int(d["graph_max_neighbor"]),
+        residue_loc_is_alphac=bool(d["graph_residue_loc_is_alphac"]),
+        pad_token_id=int(d.get("pad_token_id", 4097)), weight_dir=str(m.get("weight_paths", "")))
+
+
 def tokenizer_config(codebook_size: int = 4096, df: int = 1) -> TokenizerConfig:
     if (codebook_size, df) not in SHIPPED:
         raise ValueError(f"no shipped model for codebook_size={codebook_size}, df={df}")

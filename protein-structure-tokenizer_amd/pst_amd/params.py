@@ -36,19 +36,87 @@ def param_spec(codes_dim: int = 6, n_block: int = 3, n_layer: int = 3) -> List[T
             s += [(f"{p}/edge_mlp/~/linear_{i}", "w", (fi, fo)), (f"{p}/edge_mlp/~/linear_{i}", "b", (fo,))]
         for nm in ("norm_msg", "norm_msg_1", "norm_msg_2"):
             s += [(f"{p}/{nm}", "scale", (H,)), (f"{p}/{nm}", "offset", (H,))]
-    B = n_block
+    s += _scaler_spec(DS, n_block)
+    s += [("vq3_d/down_proj", "w", (H, codes_dim)), ("vq3_d/down_proj", "b", (codes_dim,))]
+    return s
+
+
+US = "vq3_d/~/cross_attn_upsampling"
+SEQ = "vq3_d/~/sequence_decoder"
+SM = "vq3_d/~/structure_module"
+
+
+def _scaler_spec(root: str, B: int) -> List[Tuple[str, str, Tuple[int, ...]]]:
+    s: List[Tuple[str, str, Tuple[int, ...]]] = []
     for nm in ("query_norm", "data_norm"):
-        s += [(f"{DS}/cross_attention/{nm}", "scale", (B, H)), (f"{DS}/cross_attention/{nm}", "offset", (B, H))]
-    att = f"{DS}/cross_attention/attention"
+        s += [(f"{root}/cross_attention/{nm}", "scale", (B, H)), (f"{root}/cross_attention/{nm}", "offset", (B, H))]
+    att = f"{root}/cross_attention/attention"
     for w in ("query_w", "key_w", "value_w", "gating_w"):
         s += [(att, w, (B, H, 4, 32))]
     s += [(att, "gating_b", (B, 4, 32)), (att, "output_w", (B, 4, 32, H)), (att, "output_b", (B, H))]
     for tr in ("resampled_transition", "original_transition"):
-        s += [(f"{DS}/{tr}/input_layer_norm", "scale", (B, H)), (f"{DS}/{tr}/input_layer_norm", "offset", (B, H))]
-        s += [(f"{DS}/{tr}/transition1", "weights", (B, H, 2 * H)), (f"{DS}/{tr}/transition1", "bias", (B, 2 * H))]
-        s += [(f"{DS}/{tr}/transition2", "weights", (B, 2 * H, H)), (f"{DS}/{tr}/transition2", "bias", (B, H))]
-    s += [("vq3_d/down_proj", "w", (H, codes_dim)), ("vq3_d/down_proj", "b", (codes_dim,))]
+        s += [(f"{root}/{tr}/input_layer_norm", "scale", (B, H)), (f"{root}/{tr}/input_layer_norm", "offset", (B, H))]
+        s += [(f"{root}/{tr}/transition1", "weights", (B, H, 2 * H)), (f"{root}/{tr}/transition1", "bias", (B, 2 * H))]
+        s += [(f"{root}/{tr}/transition2", "weights", (B, 2 * H, H)), (f"{root}/{tr}/transition2", "bias", (B, H))]
     return s
+
+
+def _lin(mod: str, fi: int, fo: int, w: str = "weights", b: str = "bias"):
+    return [(mod, w, (fi, fo)), (mod, b, (fo,))]
+
+
+def _ln(mod: str, n: int = H):
+    return [(mod, "scale", (n,)), (mod, "offset", (n,))]
+
+
+def decoder_param_spec(codes_dim: int = 6, n_block: int = 3) -> List[Tuple[str, str, Tuple[int, ...]]]:
+    """Decoder-half tensors (`Vq3D.decode_and_make_structure`, model/model.py:481-570).
+
+    Not used by the tokenize path; listed so a full `params.npz` (189 leaves) can be split by
+    leaf order. Names/shapes: tests/golden/full_param_names.json (reference model initialised
+    under the test shim, see tests/golden/make_param_names.py).
+    """
+    S = 384
+    s = _lin("vq3_d/up_proj", codes_dim, H, "w", "b")
+    s += _scaler_spec(f"{US}/cross_attn_scaler_iteration", n_block)
+    s += _lin(f"{US}/linear_proj_original", 2 * H, H, "w", "b")
+    s += _lin(f"{SEQ}/linear", 2 * H, H, "w", "b")
+    s += _ln(f"{SEQ}/pair_transition_init/input_layer_norm")
+    s += _lin(f"{SEQ}/pair_transition_init/transition1", H, 2 * H)
+    s += _lin(f"{SEQ}/pair_transition_init/transition2", 2 * H, H)
+    pr = f"{SEQ}/pairwise_representation"
+    s += _ln(f"{pr}/layer_norm_input") + _ln(f"{pr}/layer_norm_output")
+    s += _lin(f"{pr}/left_projection", H, 2 * H) + _lin(f"{pr}/right_projection", H, 2 * H)
+    s += _lin(f"{pr}/right_projection_1", 2 * H, H)
+    s += _lin(f"{pr}/output_projection_layer1", 2 * H, 2 * H) + _lin(f"{pr}/output_projection_layer2", 2 * H, H)
+    fi = f"{SM}/fold_iteration"
+    s += _lin(f"{fi}/affine_update", S, 6) + _ln(f"{fi}/attention_layer_norm", S)
+    ipa = f"{fi}/invariant_point_attention"
+    s += [(ipa, "trainable_point_weights", (12,))]
+    s += _lin(f"{ipa}/attention_2d", H, 12) + _lin(f"{ipa}/kv_point_local", S, 432)
+    s += _lin(f"{ipa}/kv_scalar", S, S) + _lin(f"{ipa}/output_projection", 2112, S)
+    s += _lin(f"{ipa}/q_point_local", S, 144) + _lin(f"{ipa}/q_scalar", S, 192)
+    rs = f"{fi}/rigid_sidechain"
+    s += _lin(f"{rs}/input_projection", S, H) + _lin(f"{rs}/input_projection_1", H, H)
+    for r in ("resblock1", "resblock1_1", "resblock2", "resblock2_1"):
+        s += _lin(f"{rs}/{r}", H, H)
+    s += _lin(f"{rs}/unnormalized_angles", H, 6)
+    for t in ("transition", "transition_1", "transition_2"):
+        s += _lin(f"{fi}/{t}", S, S)
+    s += _ln(f"{fi}/transition_layer_norm", S)
+    s += _lin(f"{SM}/initial_projection", H, S) + _ln(f"{SM}/pair_layer_norm") + _ln(f"{SM}/single_layer_norm")
+    return s
+
+
+def full_param_spec(codes_dim: int = 6) -> List[Tuple[str, str, Tuple[int, ...]]]:
+    """Every leaf of a Vq3D checkpoint in JAX dict-flatten order (sorted module, sorted name).
+
+    This is the leaf order of `params.npz` (`scripts/inference_runner.py:146-149` unflattens
+    `uploaded.files` in order against the checkpoint's treedef; `ForwardVQ3D` wraps exactly one
+    `Vq3D`, model/model.py:575-624, so its `forward_vq3_d/` prefix does not change the order).
+    """
+    s = param_spec(codes_dim) + decoder_param_spec(codes_dim)
+    return sorted(s, key=lambda t: (t[0], t[1]))
 
 
 def param_count(codes_dim: int = 6) -> int:
@@ -110,6 +178,16 @@ def random_params(codes_dim: int = 6, seed: int = 0, z_scale: float = 1.5) -> Di
     return out
 
 
+def random_full_params(codes_dim: int = 6, seed: int = 0) -> Dict[str, Dict[str, np.ndarray]]:
+    """A whole Vq3D checkpoint's worth of random tensors (encoder as `random_params`, decoder
+    N(0, 0.02²)) — stands in for a real `params.npz`, which is not available offline."""
+    out = random_params(codes_dim, seed)
+    rng = np.random.default_rng(seed + 1)
+    for mod, name, shape in decoder_param_spec(codes_dim):
+        out.setdefault(mod, {})[name] = (0.02 * rng.standard_normal(shape)).astype(np.float32)
+    return out
+
+
 def random_blob(codes_dim: int = 6, seed: int = 0) -> np.ndarray:
     return pack(random_params(codes_dim, seed), codes_dim)
 
@@ -122,25 +200,54 @@ def params_keys_conversion(dict_params: Dict, key_name: str = "forward_vq3_d/") 
     return dict_params
 
 
-def load_params_npz(filename: str, names: List[Tuple[str, str]]) -> Dict[str, Dict[str, np.ndarray]]:
-    """`params.npz` (leaves `arr_0..`, JAX dict-flatten order = sorted keys) → nested dict.
+def load_params_npz(filename: str, names=None, codes_dim=None, convert: bool = True
+                    ) -> Dict[str, Dict[str, np.ndarray]]:
+    """`params.npz` → nested haiku-style dict. Mirror of `scripts/inference_runner.py:136-150`.
 
-    `names` is the full ordered (module, param) list of the checkpoint's tree (the pickled
-    jaxlib PyTreeDef in `state_variables.npy` is not unpickled here). Mirror of
-    `scripts/inference_runner.py:136-150` without `jax.tree_util.tree_unflatten`.
+    The reference unflattens the arrays, in `uploaded.files` order, against the PyTreeDef
+    pickled in `state_variables.npy`. That pickle is never loaded here (only loaders that
+    execute nothing from the file are used); the tree is instead `names` (ordered
+    (module, param) pairs), by default `full_param_spec(codes_dim)` — the leaf order JAX
+    gives a Vq3D params dict; `codes_dim` defaults to the length of the first leaf
+    (`vq3_d/down_proj/b`). An npz keyed `module:param` (`save_params_npz(..., named=True)`)
+    is read by name. Every array's shape is checked against the spec; `convert` applies
+    `params_keys_conversion` as `InferenceRunner.load_params` does.
     """
     with np.load(filename, allow_pickle=False) as f:
-        files = sorted(f.files, key=lambda s: int(s.split("_")[1]) if s.startswith("arr_") else s)
-        if len(files) != len(names):
-            raise ValueError(f"{filename}: {len(files)} arrays but {len(names)} names")
+        files = list(f.files)
         out: Dict[str, Dict[str, np.ndarray]] = {}
-        for (mod, name), fn in zip(names, files):
-            out.setdefault(mod, {})[name] = np.asarray(f[fn])
-    return params_keys_conversion(out)
+        if files and all(":" in k for k in files):
+            for k in files:
+                mod, name = k.rsplit(":", 1)
+                out.setdefault(mod, {})[name] = np.asarray(f[k])
+        else:
+            if names is None:
+                if codes_dim is None:
+                    codes_dim = int(f[files[0]].shape[0]) if files and f[files[0]].ndim == 1 else 6
+                names = [(m, p) for m, p, _ in full_param_spec(codes_dim)]
+            if len(files) != len(names):
+                raise ValueError(f"{filename}: {len(files)} arrays but the tree has {len(names)} leaves")
+            for (mod, name), fn in zip(names, files):
+                out.setdefault(mod, {})[name] = np.asarray(f[fn])
+    conv = params_keys_conversion(dict(out))
+    if codes_dim is None:
+        b = conv.get("vq3_d/down_proj", {}).get("b")
+        codes_dim = int(b.shape[0]) if b is not None else 6
+    spec = {(m, p): sh for m, p, sh in full_param_spec(codes_dim)}
+    for mod, d in conv.items():
+        for name, a in d.items():
+            want = spec.get((mod, name))
+            if want is not None and tuple(a.shape) != tuple(want):
+                raise ValueError(f"{filename}: {mod}/{name} has shape {a.shape}, expected {want}")
+    return conv if convert else out
 
 
-def save_params_npz(filename: str, params: Dict[str, Dict[str, np.ndarray]]) -> List[Tuple[str, str]]:
-    """Write params in the reference's npz leaf order (sorted module, then sorted param)."""
+def save_params_npz(filename: str, params: Dict[str, Dict[str, np.ndarray]], named: bool = False) -> List[Tuple[str, str]]:
+    """Write params in the reference's npz leaf order (sorted module, then sorted param):
+    `arr_0..` like a flattened JAX tree, or keyed `module:param` when `named`."""
     names = [(m, p) for m in sorted(params) for p in sorted(params[m])]
-    np.savez(filename, *[params[m][p] for m, p in names])
+    if named:
+        np.savez(filename, **{f"{m}:{p}": params[m][p] for m, p in names})
+    else:
+        np.savez(filename, *[params[m][p] for m, p in names])
     return names

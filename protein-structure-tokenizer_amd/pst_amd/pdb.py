@@ -121,3 +121,26 @@ def protein_structure_from_pdb_string(pdb_str: str, chain_id: Optional[str] = No
 def protein_structure_from_pdb_file(path: str) -> ProteinStructureSample:
     with open(path, "r") as fh:
         return protein_structure_from_pdb_string(fh.read())
+
+
+def to_pdb_string(sample: ProteinStructureSample, chain_id: str = "A") -> str:
+    """Minimal ATOM-record writer (the fields the parser above reads): one residue per row of
+    `sample`, atoms present in `atom37_gt_exists`, coordinates %8.3f. Used to build PDB inputs
+    for end-to-end CLI tests; the reference's full writer (`data/protein.py:to_pdb`) belongs to
+    the decode path."""
+    lines = []
+    serial = 1
+    aat = np.argmax(sample.aatype, axis=-1) if sample.aatype.size else np.zeros(sample.nb_residues, int)
+    for i in range(sample.nb_residues):
+        a = int(aat[i])
+        resname = rc.restype_1to3.get(rc.restypes[a], "UNK") if a < rc.restype_num else "UNK"
+        for j, name in enumerate(rc.atom_types):
+            if not sample.atom37_gt_exists[i, j]:
+                continue
+            x, y, z = (float(v) for v in sample.atom37_positions[i, j])
+            nm = name if len(name) == 4 else " " + name
+            lines.append(f"ATOM  {serial:5d} {nm:<4s} {resname:>3s} {chain_id}{i + 1:4d}    "
+                         f"{x:8.3f}{y:8.3f}{z:8.3f}{1.0:6.2f}{0.0:6.2f}          {name[0]:>2s}")
+            serial += 1
+    lines.append("END")
+    return "\n".join(lines) + "\n"

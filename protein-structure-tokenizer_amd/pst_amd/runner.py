@@ -1,0 +1,257 @@
+"""Host-side mirror of the reference's tokenize runner (`scripts/inference_runner.py`).
+
+Same names, argument meaning and error behaviour as the reference, with the compute moved
+into libpst (`include/pst.h`):
+
+  reference (JAX / haiku, pmap over local devices)      here (libpst contexts, one per GPU)
+  ----------------------------------------------------  -------------------------------------
+  make_graph_from_pdb  (:40-74)  parse + size gates +   parse + the same size gates; the graph
+                       preprocess_sample on the host    itself is built on the GPU (k_prep/k_knn)
+  batch_collate        (:77-83)  stack padded graphs    pack ragged atom37 arrays + offsets
+  load_params          (:136-150) npz + pickled treedef npz + leaf order of full_param_spec
+  params_keys_conversion (:153-165)                     same (pst_amd.params)
+  InferenceRunner.prepare_devices (:169-177)            HIP devices (backend "gpu" only)
+  InferenceRunner.prepare_tokenize_fn (:179-191)        TokenizeFn: per-device libpst contexts
+  InferenceRunner.load_params (:236-248)                ReplicatedParams
+  InferenceRunner.tokenize (:250-324)                   same loop, files and layout
+
+There is no CPU fallback: `backend` must be "gpu" (the reference's "cpu"/"tpu" backends are
+XLA targets this library does not have) and libpst.so must load.
+"""
+import concurrent.futures as _cf
+import logging
+import os
+import time
+from itertools import cycle, islice
+from typing import Any, Callable, Dict, List, NamedTuple, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import _native
+from . import params as _params
+from .config import LEVELS, TokenizerConfig
+from .pdb import protein_structure_from_pdb_string
+from .sample import ProteinStructureSample
+
+
+# ------------------------------------------------------------------------------- graph inputs
+def make_graph_from_pdb(pdb_file_path: str, num_neighbor: int, downsampling_ratio: int,
+                        residue_loc_is_alphac: bool, padding_num_residue: int) -> ProteinStructureSample:
+    """Parse one PDB and apply the reference's size gates (`inference_runner.py:40-74`).
+
+    Returns the parsed structure; the residue graph (`preprocess_sample`) is built on the GPU
+    by `pst_tokenize`, so nothing else happens on the host. `residue_loc_is_alphac=False` and
+    other `padding_num_residue` / `num_neighbor` values than the shipped 512 / 50 are rejected
+    (the device kernels are specialised for them).
+    """
+    with open(pdb_file_path, "r") as file:
+        pdb_content = file.read()
+    sample = protein_structure_from_pdb_string(pdb_content)
+    if sample.nb_residues > 512:
+        raise NotImplementedError(
+            "We currently don't support protein with more than 512 residues"
+            f"given: {sample.nb_residues}")
+    if sample.nb_residues < num_neighbor:
+        raise NotImplementedError(
+            f"We currently don't support protein with less than {num_neighbor} residues"
+            f"given: {sample.nb_residues}")
+    if not residue_loc_is_alphac:
+        raise NotImplementedError("libpst builds the graph on C-alpha locations only "
+                                  "(graph_residue_loc_is_alphac: true in every shipped config)")
+    if num_neighbor != 50 or padding_num_residue != 512:
+        raise NotImplementedError("libpst is specialised for graph_max_neighbor=50, seq_max_size=512")
+    if downsampling_ratio not in (1, 2, 4):
+        raise ValueError(f"downsampling_ratio must be 1, 2 or 4, got {downsampling_ratio}")
+    return sample
+
+
+class ProteinBatch(NamedTuple):
+    """A collated batch: `batch_dims` = [num_device, batch_size_per_device] (or any shape) over
+    a flat list of structures, packed per leading index for the device calls."""
+    batch_dims: Tuple[int, ...]
+    samples: Tuple[ProteinStructureSample, ...]
+
+    def shard(self, i: int) -> List[ProteinStructureSample]:
+        per = int(np.prod(self.batch_dims[1:])) if len(self.batch_dims) > 1 else 1
+        return list(self.samples[i * per:(i + 1) * per])
+
+
+def batch_collate(batch_dims: List[int], batch_of_samples: List[ProteinStructureSample]) -> ProteinBatch:
+    """Mirror of `inference_runner.py:77-83` (same count check as the reshape there)."""
+    if int(np.prod(batch_dims)) != len(batch_of_samples):
+        raise ValueError(f"cannot reshape {len(batch_of_samples)} samples into {list(batch_dims)}")
+    return ProteinBatch(tuple(int(b) for b in batch_dims), tuple(batch_of_samples))
+
+
+# ------------------------------------------------------------------------------------ params
+def load_params(filename: str, tree_def: Optional[Sequence[Tuple[str, str]]] = None,
+                codes_dim: Optional[int] = None) -> Dict[str, Dict[str, np.ndarray]]:
+    """Mirror of `inference_runner.py:136-150`. `tree_def` is the ordered (module, param) leaf
+    list; by default the full Vq3D tree (`params.full_param_spec`). Prefix not stripped."""
+    return _params.load_params_npz(filename, tree_def, codes_dim=codes_dim, convert=False)
+
+
+params_keys_conversion = _params.params_keys_conversion
+
+
+class ReplicatedParams:
+    """What `jax.device_put_replicated(params, devices)` returns in the reference: the same
+    parameters for every local device. Device copies live in the libpst contexts TokenizeFn
+    creates on first use."""
+
+    def __init__(self, params: Dict[str, Dict[str, np.ndarray]], devices: Sequence[int]):
+        self.params = params
+        self.devices = list(devices)
+        self.codes_dim = int(np.asarray(params["vq3_d/down_proj"]["b"]).shape[0])
+        self.blob = _params.pack(params, self.codes_dim)
+
+
+# -------------------------------------------------------------------------------- tokenize fn
+def pad_token_value(levels: Sequence[int]) -> int:
+    """Token id of a masked (padding) row: bounded = 0 → code 0 → Σ (L//2)·basis
+    (`model/quantize.py:183-209`)."""
+    basis = np.concatenate(([1], np.cumprod(levels[:-1])))
+    return int(sum((l // 2) * b for l, b in zip(levels, basis)))
+
+
+class TokenizeFn:
+    """`jax.pmap(hk.transform(encode_and_quantize).apply)` for libpst.
+
+    `fn(model_params, random_key, batched_graph)` runs shard i of `batched_graph` on
+    `devices[i]` (one host thread per device; the C calls release the GIL) and returns a dict
+    with "tokens" uint32 [*batch_dims, seq_max_size // df] (padding rows carry the padded-token
+    id exactly as the reference's output does) and "n_tokens" int32 [*batch_dims]
+    (= tokens_mask.sum(-1) of the reference graph). `random_key` is accepted and unused, as in
+    the reference's inference path (no stochastic op when is_training=False).
+    """
+
+    def __init__(self, cfg: TokenizerConfig, devices: Sequence[int]):
+        self.cfg = cfg
+        self.devices = list(devices)
+        self._ctx: Dict[Tuple[int, int], _native.Tokenizer] = {}
+        self._pool = _cf.ThreadPoolExecutor(max_workers=max(1, len(self.devices)))
+
+    def _context(self, model_params: ReplicatedParams, dev: int) -> _native.Tokenizer:
+        key = (id(model_params), dev)
+        t = self._ctx.get(key)
+        if t is None:
+            levels = self.cfg.levels
+            if len(levels) != model_params.codes_dim:
+                raise ValueError(f"params have codes_dimension {model_params.codes_dim}, config levels {levels}")
+            t = _native.Tokenizer(dev, self.cfg.codebook_size, self.cfg.downsampling_ratio,
+                                  model_params.blob, levels)
+            self._ctx[key] = t
+        return t
+
+    def __call__(self, model_params: ReplicatedParams, random_key: Any, batched_graph: ProteinBatch) -> Dict[str, np.ndarray]:
+        n_dev = batched_graph.batch_dims[0]
+        if n_dev > len(self.devices):
+            raise ValueError(f"batch has {n_dev} device shards but only {len(self.devices)} devices")
+        out_len = self.cfg.seq_max_size // self.cfg.downsampling_ratio
+        pad = pad_token_value(self.cfg.levels)
+
+        def run(i):
+            shard = batched_graph.shard(i)
+            t = self._context(model_params, self.devices[i])
+            pos, flags, off = _native.pack_samples(shard)
+            tok, nt, _ = t.tokenize_packed(pos, flags, off)
+            rows = np.full((len(shard), out_len), pad, np.uint32)
+            for b in range(len(shard)):
+                rows[b, :nt[b]] = tok[off[b]:off[b] + nt[b]]
+            return rows, nt
+
+        res = list(self._pool.map(run, range(n_dev)))
+        tokens = np.stack([r for r, _ in res]).reshape(*batched_graph.batch_dims, out_len)
+        n_tokens = np.stack([n for _, n in res]).reshape(*batched_graph.batch_dims)
+        return {"tokens": tokens, "n_tokens": n_tokens}
+
+    def close(self):
+        for t in self._ctx.values():
+            t.close()
+        self._ctx.clear()
+        self._pool.shutdown(wait=True)
+
+
+# ------------------------------------------------------------------------------------- runner
+def hip_device_count() -> int:
+    return _native.device_count()
+
+
+class InferenceRunner:
+    @staticmethod
+    def prepare_devices(backend: str = "gpu"):
+        """(`inference_runner.py:169-177`) → (local device ordinals, count)."""
+        if backend != "gpu":
+            raise NotImplementedError(
+                f"backend {backend!r}: libpst runs the tokenize path on MI355X GPUs only (backend='gpu')")
+        n = hip_device_count()
+        if n < 1:
+            raise RuntimeError("no HIP device visible")
+        rank = int(os.environ.get("RANK", "0"))
+        if rank == 0:
+            print("---Devices---\n" + f"\tlocal device count: {n}")
+        return list(range(n)), n
+
+    @staticmethod
+    def prepare_tokenize_fn(cfg: TokenizerConfig, devices: Sequence[int]) -> Callable:
+        return TokenizeFn(cfg, devices)
+
+    @staticmethod
+    def load_params(model_dir: str, local_devices: Sequence[int]) -> ReplicatedParams:
+        """(`inference_runner.py:236-248`). Reads `model_dir/params.npz` only: the pickled
+        treedef in `state_variables.npy` is never unpickled (the leaf order is
+        `params.full_param_spec`, the order JAX flattens the Vq3D params dict in)."""
+        path = os.path.join(model_dir, "params.npz")
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        p = _params.load_params_npz(path)
+        return ReplicatedParams(p, local_devices)
+
+    @staticmethod
+    def tokenize(random_key: Any, quantize: Callable, model_params: ReplicatedParams, pdbs: List[str],
+                 token_save_path: str, num_device: int, data_config: TokenizerConfig,
+                 batch_size_per_device: int = 8, logger: Optional[logging.Logger] = None):
+        """(`inference_runner.py:250-324`): same batching (list cycled up to a multiple of
+        num_device × batch_size_per_device), same output files: one
+        `<pdb stem>_tokens.npy` per PDB, uint32 [1, n_tokens]. PDB parsing of the next batch
+        overlaps the GPU work of the current one."""
+        if logger is not None:
+            logger.info(f"Starting tokenization of {pdbs}")
+        os.makedirs(token_save_path, exist_ok=False)
+        effective_batch_size = batch_size_per_device * num_device
+        num_iteration = len(pdbs) // effective_batch_size + int((len(pdbs) % effective_batch_size) > 0)
+        total = num_iteration * effective_batch_size
+        pdbs = list(islice(cycle(pdbs), total))
+
+        def load(it):
+            files = pdbs[it * effective_batch_size:(it + 1) * effective_batch_size]
+            graphs = [make_graph_from_pdb(pdb_file_path=f, num_neighbor=data_config.graph_max_neighbor,
+                                          downsampling_ratio=data_config.downsampling_ratio,
+                                          residue_loc_is_alphac=data_config.residue_loc_is_alphac,
+                                          padding_num_residue=data_config.seq_max_size) for f in files]
+            return files, batch_collate([num_device, batch_size_per_device], graphs)
+
+        with _cf.ThreadPoolExecutor(max_workers=1) as io:
+            nxt = io.submit(load, 0) if num_iteration else None
+            for it in range(num_iteration):
+                files, batched = nxt.result()
+                if it + 1 < num_iteration:
+                    nxt = io.submit(load, it + 1)
+                start_time = time.perf_counter()
+                out = quantize(model_params, random_key, batched)
+                tokens = out["tokens"].reshape(effective_batch_size, -1)
+                n_tok = out["n_tokens"].reshape(effective_batch_size)
+                for seq_id in range(effective_batch_size):
+                    token_array = tokens[seq_id].reshape(1, -1)[:, :n_tok[seq_id]]
+                    filename = os.path.basename(files[seq_id]).split(".pdb")[0]
+                    np.save(os.path.join(token_save_path, filename + "_tokens"), token_array)
+                if logger is not None:
+                    logger.info(f"Took {time.perf_counter() - start_time}s to tokenize")
+
+
+def shard_for_rank(items: Sequence[Any], rank: int, world_size: int) -> List[Any]:
+    """Round-robin partition of independent proteins across ranks (one process per GPU, no
+    data-path collective): rank r takes items r, r+W, r+2W, ..."""
+    if not 0 <= rank < world_size:
+        raise ValueError(f"rank {rank} outside world of {world_size}")
+    return list(items[rank::world_size])

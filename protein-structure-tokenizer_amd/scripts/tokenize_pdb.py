@@ -1,0 +1,96 @@
+"""Tokenize a directory of PDB files — drop-in for the reference's `scripts/tokenize_pdb.py`.
+
+    python protein-structure-tokenizer_amd/scripts/tokenize_pdb.py \\
+        --pdb_dir DIR --token_save_path OUT [--codebook_size 4096] [--model_downsampling 1] \\
+        [--batch_size_per_device 1] [--weights_dir weights/4k_df_1/] [--config_path CFG]
+
+Same arguments and outputs (`OUT/<pdb stem>_tokens.npy`, uint32 [1, n_tokens]) as the
+reference (`scripts/tokenize_pdb.py:79-121`); `--backend` accepts only "gpu" (the default
+here). The model directory must hold `params.npz` (read with `allow_pickle=False`; the pickled
+`state_variables.npy` is not needed). Without `--config_path` the shipped hyper-parameters are
+used directly (`pst_amd.config.tokenizer_config`); with it, the reference's YAML tree is
+composed the same way the reference does (`config_overrides` from the two flags).
+
+One process drives every local GPU (a host thread per GPU, like the reference's pmap). Under
+`torchrun` (WORLD_SIZE > 1) each rank instead takes GPU LOCAL_RANK and a round-robin shard of
+the PDB list; there is no collective on the data path.
+"""
+import argparse
+import os
+import sys
+from typing import List, Optional
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+
+from pst_amd import config as C  # noqa: E402
+from pst_amd.runner import InferenceRunner, shard_for_rank  # noqa: E402
+
+
+def main(pdbs: List[str], token_save_path: str, backend: str, batch_size_per_device: int = 8,
+         codebook_size: int = 4096, downsampling_ratio: int = 1, weights_dir: Optional[str] = None,
+         config_path: Optional[str] = None, config_overrides: Optional[List[str]] = None):
+    if config_path:
+        cfg = C.config_from_hydra(C.load_config("vq3d_inference", job_name="tokenize",
+                                                overrides=config_overrides, config_path=config_path))
+    else:
+        cfg = C.tokenizer_config(codebook_size, downsampling_ratio)
+    runner = InferenceRunner()
+    local_devices, n_local_device = runner.prepare_devices(backend=backend)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        rank = int(os.environ.get("RANK", "0"))
+        local_devices = [int(os.environ.get("LOCAL_RANK", "0"))]
+        pdbs = shard_for_rank(sorted(pdbs), rank, world)
+        if not pdbs:
+            return
+    tokenize = runner.prepare_tokenize_fn(cfg=cfg, devices=local_devices)
+    model_params = runner.load_params(model_dir=weights_dir or cfg.weight_dir, local_devices=local_devices)
+    try:
+        if world > 1:
+            _tokenize_rank(runner, tokenize, model_params, pdbs, token_save_path, cfg, batch_size_per_device)
+        else:
+            runner.tokenize(random_key=None, quantize=tokenize, model_params=model_params, pdbs=pdbs,
+                            token_save_path=token_save_path, num_device=len(local_devices),
+                            data_config=cfg, batch_size_per_device=batch_size_per_device)
+    finally:
+        tokenize.close()
+
+
+def _tokenize_rank(runner, tokenize, model_params, pdbs, token_save_path, cfg, bs):
+    # every rank writes into the same directory; rank files are disjoint by construction
+    os.makedirs(token_save_path, exist_ok=True)
+    tmp = os.path.join(token_save_path, f".rank{os.environ.get('RANK', '0')}")
+    runner.tokenize(random_key=None, quantize=tokenize, model_params=model_params, pdbs=pdbs,
+                    token_save_path=tmp, num_device=1, data_config=cfg, batch_size_per_device=bs)
+    for f in os.listdir(tmp):
+        os.replace(os.path.join(tmp, f), os.path.join(token_save_path, f))
+    os.rmdir(tmp)
+
+
+def cli(argv=None):
+    parser = argparse.ArgumentParser(description="Tokenizer specification !")
+    parser.add_argument("--model_downsampling", type=int, choices=[1, 2, 4], default=1)
+    parser.add_argument("--codebook_size", type=int, choices=[432, 1728, 4096, 64000], default=4096)
+    parser.add_argument("--token_save_path", type=str, required=True)
+    parser.add_argument("--pdb_dir", type=str, required=True, help="folder containing the .pdb files to be tokenized")
+    parser.add_argument("--backend", type=str, default="gpu", choices=["gpu", "tpu", "cpu"])
+    parser.add_argument("--batch_size_per_device", type=int, default=1)
+    parser.add_argument("--weights_dir", type=str, default=None,
+                        help="model directory holding params.npz (default: the config's weight_paths)")
+    parser.add_argument("--config_path", type=str, default=None,
+                        help="the reference's config/structure_tokenizer tree (optional)")
+    args = parser.parse_args(argv)
+    df = args.model_downsampling
+    if (args.codebook_size, df) not in C.SHIPPED:
+        raise SystemExit(f"no model for codebook_size={args.codebook_size}, df={df}")
+    pdbs = [os.path.join(args.pdb_dir, f) for f in os.listdir(args.pdb_dir)]
+    main(pdbs=pdbs, token_save_path=args.token_save_path, backend=args.backend,
+         batch_size_per_device=args.batch_size_per_device, codebook_size=args.codebook_size,
+         downsampling_ratio=df, weights_dir=args.weights_dir, config_path=args.config_path,
+         config_overrides=C.overrides_for(args.codebook_size, df))
+
+
+if __name__ == "__main__":
+    cli()

@@ -1,0 +1,36 @@
+"""Worker for test_multirank.py (one process per rank, gloo on 127.0.0.1)."""
+import os
+import sys
+
+
+def run(rank, world, port, pdb_dir, model_dir, out_dir, result_q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (root, os.path.join(root, "protein-structure-tokenizer_amd"), here):
+        sys.path.insert(0, p)
+    import numpy as np
+    import torch.distributed as dist
+    from pst_amd import runner
+    from test_host import OracleTokenizeFn
+
+    sys.path.insert(0, os.path.join(root, "protein-structure-tokenizer_amd", "scripts"))
+    import tokenize_pdb as cli
+
+    # the per-GPU device query and compute are swapped for the CPU oracle; the CLI's rank
+    # sharding, file handling and runner loop are the product code
+    runner.InferenceRunner.prepare_devices = staticmethod(lambda backend="gpu": ([0], 1))
+    runner.InferenceRunner.prepare_tokenize_fn = staticmethod(lambda cfg, devices: OracleTokenizeFn(cfg, devices))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pdbs = [os.path.join(pdb_dir, f) for f in os.listdir(pdb_dir)]
+    mine = runner.shard_for_rank(sorted(pdbs), rank, world)
+    cli.main(pdbs=pdbs, token_save_path=out_dir, backend="gpu", batch_size_per_device=2,
+             codebook_size=4096, downsampling_ratio=1, weights_dir=model_dir)
+    # host-side gather of what each rank handled (test bookkeeping only, not the data path)
+    got = [None] * world
+    dist.all_gather_object(got, sorted(os.path.basename(p) for p in mine))
+    dist.barrier()
+    if rank == 0:
+        result_q.put(got)
+    dist.destroy_process_group()

@@ -32,3 +32,7 @@ def softmax(x, axis=-1):
 def one_hot(x, num_classes, dtype=_np.float64):
     x = _np.asarray(x)
     return (x[..., None] == _np.arange(num_classes)).astype(dtype)
+
+
+def softplus(x):
+    return _np.logaddexp(x, 0)

@@ -1,0 +1,56 @@
+"""End to end on the GPU: the drop-in CLI (`scripts/tokenize_pdb.py`) and `InferenceRunner`
+through libpst, checked against the CPU oracle token for token."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pst_amd import config as C
+from pst_amd import params as P
+from pst_amd import pdb, runner, synthetic
+
+pytestmark = pytest.mark.gpu
+SCRIPTS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "protein-structure-tokenizer_amd", "scripts")
+
+
+@pytest.mark.parametrize("cb,df", [(4096, 1), (64000, 4)])
+def test_cli_end_to_end(tmp_path, cb, df):
+    sys.path.insert(0, SCRIPTS)
+    import tokenize_pdb
+    D = len(C.LEVELS[cb])
+    pdb_dir = tmp_path / "pdbs"
+    pdb_dir.mkdir()
+    ss = {f"s{i}": synthetic.synthetic_protein(n, 300 + i) for i, n in enumerate((50, 77, 130, 256, 512))}
+    for k, s in ss.items():
+        (pdb_dir / f"{k}.pdb").write_text(pdb.to_pdb_string(s))
+    mdir = tmp_path / "model"
+    mdir.mkdir()
+    full = P.random_full_params(D, seed=5)
+    P.save_params_npz(str(mdir / "params.npz"), full)
+    out = tmp_path / "tokens"
+    tokenize_pdb.cli(["--pdb_dir", str(pdb_dir), "--token_save_path", str(out), "--codebook_size", str(cb),
+                      "--model_downsampling", str(df), "--batch_size_per_device", "2", "--weights_dir", str(mdir)])
+    blob = P.pack(full, D)
+    for k, s in ss.items():
+        t = np.load(out / f"{k}_tokens.npy")
+        want = O.tokenize(blob, C.LEVELS[cb], df, s.atom37_positions, s.atom_flags())["tokens"]
+        assert t.dtype == np.uint32 and t.shape == (1, s.nb_residues // df)
+        assert np.array_equal(t[0], want), k
+
+
+def test_tokenize_fn_on_gpu_matches_reference_layout():
+    cfg = C.tokenizer_config(4096, 1)
+    devs, n = runner.InferenceRunner.prepare_devices("gpu")
+    mp = runner.ReplicatedParams(P.random_params(6, 9), devs[:1])
+    fn = runner.InferenceRunner.prepare_tokenize_fn(cfg, devs[:1])
+    ss = [synthetic.synthetic_protein(m, 17 + m) for m in (51, 199, 64)]
+    out = fn(mp, None, runner.batch_collate([1, 3], ss))
+    fn.close()
+    assert out["tokens"].shape == (1, 3, 512)
+    for b, s in enumerate(ss):
+        want = O.tokenize(mp.blob, cfg.levels, 1, s.atom37_positions, s.atom_flags())["tokens"]
+        assert np.array_equal(out["tokens"][0, b, :s.nb_residues], want)
+        assert np.all(out["tokens"][0, b, s.nb_residues:] == runner.pad_token_value(cfg.levels))

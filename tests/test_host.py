@@ -1,0 +1,210 @@
+"""Host logic on CPU: PDB parser semantics, size gates, batching/collation, the runner's file
+layout and the multi-rank sharding. The per-device compute is swapped for the CPU oracle in a
+test-only subclass (libpst needs a GPU); everything else is the product code."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pst_amd import config as C
+from pst_amd import params as P
+from pst_amd import pdb, runner, synthetic
+from pst_amd.sample import ProteinStructureSample
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+# ------------------------------------------------------------------------------ PDB parser
+def _atom(serial, name, resname, chain, resseq, x, y, z, occ=1.0, altloc=" ", rec="ATOM  ", icode=" "):
+    nm = name if len(name) == 4 else " " + name
+    return (f"{rec}{serial:5d} {nm:<4s}{altloc}{resname:>3s} {chain}{resseq:4d}{icode}   "
+            f"{x:8.3f}{y:8.3f}{z:8.3f}{occ:6.2f}{0.0:6.2f}          {name[0]:>2s}")
+
+
+def _res(chain, resseq, resname="GLY", base=0.0, **kw):
+    return [_atom(1, n, resname, chain, resseq, base + i, 1.0, 2.0, **kw) for i, n in enumerate(("N", "CA", "C", "O"))]
+
+
+def test_parser_roundtrip_synthetic():
+    s = synthetic.synthetic_protein(70, 5)
+    r = pdb.protein_structure_from_pdb_string(pdb.to_pdb_string(s))
+    assert r.nb_residues == 70
+    assert np.array_equal(r.atom37_positions, s.atom37_positions)
+    assert np.array_equal(r.atom_flags(), s.atom_flags())
+    assert np.array_equal(r.aatype, s.aatype)
+
+
+def test_parser_multi_model_raises():
+    txt = "\n".join(["MODEL        1"] + _res("A", 1) + ["ENDMDL", "MODEL        2"] + _res("A", 1) + ["ENDMDL"])
+    with pytest.raises(ValueError, match="single model"):
+        pdb.protein_structure_from_pdb_string(txt)
+
+
+def test_parser_insertion_code_raises():
+    txt = "\n".join(_res("A", 1) + _res("A", 1, icode="B"))
+    with pytest.raises(ValueError, match="insertion code"):
+        pdb.protein_structure_from_pdb_string(txt)
+
+
+def test_parser_altloc_highest_occupancy_and_unk():
+    lines = _res("A", 1, "ALA")
+    lines.append(_atom(9, "CB", "ALA", "A", 1, 5.0, 5.0, 5.0, occ=0.3, altloc="A"))
+    lines.append(_atom(10, "CB", "ALA", "A", 1, 6.0, 6.0, 6.0, occ=0.7, altloc="B"))
+    lines += _res("A", 2, "MSE", base=10.0, rec="HETATM")   # non-standard → UNK
+    lines.append(_atom(20, "O", "HOH", "A", 3, 1.0, 1.0, 1.0, rec="HETATM"))  # water: O in atom37
+    lines.append(_atom(21, "ZN", "ZN", "A", 4, 1.0, 1.0, 1.0, rec="HETATM"))  # no atom37 atom → skipped
+    s = pdb.protein_structure_from_pdb_string("\n".join(lines))
+    assert s.nb_residues == 3
+    assert np.allclose(s.atom37_positions[0, 3], 6.0)  # CB index 3, altloc B
+    assert np.argmax(s.aatype, -1).tolist() == [0, 20, 20]
+    assert s.atom37_gt_exists[2].sum() == 1
+
+
+def test_parser_chain_filter_and_order():
+    txt = "\n".join(_res("B", 1) + _res("A", 1, base=5.0) + _res("B", 2, base=9.0))
+    s = pdb.protein_structure_from_pdb_string(txt)
+    assert s.nb_residues == 3
+    # Bio appends a discontinuous chain to the existing one: B1, B2, then A1
+    assert s.atom37_positions[:, 1, 0].tolist() == [1.0, 10.0, 6.0]
+    sa = pdb.protein_structure_from_pdb_string(txt, chain_id="A")
+    assert sa.nb_residues == 1
+
+
+@pytest.mark.reference
+def test_parser_casp14_fixture():
+    import glob
+    import _refenv
+    F = np.load(os.path.join(GOLD, "casp14_atom37.npz"))
+    files = sorted(glob.glob(os.path.join(_refenv.REF, "casp14_pdbs", "*.pdb")))
+    assert len(files) == len(F["names"]) == 31
+    pos = []
+    for f in files:
+        pos.append(pdb.protein_structure_from_pdb_file(f).atom37_positions)
+    assert np.array_equal(np.concatenate(pos), F["positions"].astype(np.float64))
+
+
+# ------------------------------------------------------------------------------ size gates
+def _write(tmp_path, name, s):
+    p = tmp_path / name
+    p.write_text(pdb.to_pdb_string(s))
+    return str(p)
+
+
+def test_make_graph_size_gates(tmp_path):
+    ok = _write(tmp_path, "ok.pdb", synthetic.synthetic_protein(60, 1))
+    small = _write(tmp_path, "small.pdb", synthetic.synthetic_protein(49, 1))
+    big = _write(tmp_path, "big.pdb", synthetic.synthetic_protein(513, 1))
+    kw = dict(num_neighbor=50, downsampling_ratio=1, residue_loc_is_alphac=True, padding_num_residue=512)
+    assert runner.make_graph_from_pdb(ok, **kw).nb_residues == 60
+    with pytest.raises(NotImplementedError, match="less than 50"):
+        runner.make_graph_from_pdb(small, **kw)
+    with pytest.raises(NotImplementedError, match="more than 512"):
+        runner.make_graph_from_pdb(big, **kw)
+    with pytest.raises(NotImplementedError):
+        runner.make_graph_from_pdb(ok, **dict(kw, residue_loc_is_alphac=False))
+
+
+def test_batch_collate_and_shards():
+    ss = [synthetic.synthetic_protein(50 + i, i) for i in range(6)]
+    b = runner.batch_collate([2, 3], ss)
+    assert [s.nb_residues for s in b.shard(1)] == [53, 54, 55]
+    with pytest.raises(ValueError):
+        runner.batch_collate([4, 2], ss)
+
+
+def test_pad_token_value():
+    assert runner.pad_token_value(C.LEVELS[4096]) == 2730
+    assert runner.pad_token_value(C.LEVELS[64000]) == 32036
+
+
+def test_prepare_devices_rejects_non_gpu_backends():
+    for be in ("cpu", "tpu"):
+        with pytest.raises(NotImplementedError):
+            runner.InferenceRunner.prepare_devices(be)
+
+
+# ------------------------------------------------------------------------------ configs
+@pytest.mark.reference
+@pytest.mark.parametrize("cb,df", sorted(C.SHIPPED))
+def test_hydra_config_matches_shipped_table(cb, df):
+    import _refenv
+    cfg = C.load_config("vq3d_inference", overrides=C.overrides_for(cb, df),
+                        config_path=os.path.join(_refenv.REF, "config", "structure_tokenizer"))
+    got = C.config_from_hydra(cfg)
+    want = C.tokenizer_config(cb, df)
+    assert got.levels == want.levels and got.downsampling_ratio == df
+    assert got.codebook_size == cb and got.weight_dir == want.weight_dir
+    assert (got.seq_max_size, got.graph_max_neighbor, got.residue_loc_is_alphac) == (512, 50, True)
+
+
+# ------------------------------------------------------------------------------ runner
+class _OracleCtx:
+    """Test stand-in for one libpst context: the CPU oracle behind `tokenize_packed`."""
+
+    def __init__(self, blob, levels, df):
+        self.blob, self.levels, self.df = blob, levels, df
+
+    def tokenize_packed(self, pos, flags, off):
+        tok, nt = O.tokenize_batch(self.blob, self.levels, self.df, pos, flags, off, n_threads=4)
+        return tok, nt, nt * self.df
+
+    def close(self):
+        pass
+
+
+class OracleTokenizeFn(runner.TokenizeFn):
+    def _context(self, model_params, dev):
+        return _OracleCtx(model_params.blob, self.cfg.levels, self.cfg.downsampling_ratio)
+
+
+def _oracle_tokens(blob, cfg, s):
+    return O.tokenize(blob, cfg.levels, cfg.downsampling_ratio, s.atom37_positions, s.atom_flags())["tokens"]
+
+
+@pytest.mark.parametrize("cb,df", [(4096, 1), (64000, 2)])
+def test_runner_tokenize_files(tmp_path, cb, df):
+    cfg = C.tokenizer_config(cb, df)
+    D = len(cfg.levels)
+    mdir = tmp_path / "model"
+    mdir.mkdir()
+    P.save_params_npz(str(mdir / "params.npz"), P.random_full_params(D, seed=11))
+    ss = [synthetic.synthetic_protein(n, 40 + i) for i, n in enumerate((55, 64, 81))]
+    pdbs = [_write(tmp_path, f"prot{i}.pdb", s) for i, s in enumerate(ss)]
+    R = runner.InferenceRunner
+    mp = R.load_params(str(mdir), [0, 1])
+    fn = OracleTokenizeFn(cfg, [0, 1])
+    out = str(tmp_path / "tokens")
+    R.tokenize(random_key=None, quantize=fn, model_params=mp, pdbs=pdbs, token_save_path=out,
+               num_device=2, data_config=cfg, batch_size_per_device=1)
+    assert sorted(os.listdir(out)) == [f"prot{i}_tokens.npy" for i in range(3)]
+    blob = P.pack(P.params_keys_conversion(P.random_full_params(D, seed=11)), D)
+    for i, s in enumerate(ss):
+        t = np.load(os.path.join(out, f"prot{i}_tokens.npy"))
+        assert t.dtype == np.uint32 and t.shape == (1, s.nb_residues // df)
+        assert np.array_equal(t[0], _oracle_tokens(blob, cfg, s))
+    with pytest.raises(FileExistsError):
+        R.tokenize(random_key=None, quantize=fn, model_params=mp, pdbs=pdbs, token_save_path=out,
+                   num_device=2, data_config=cfg, batch_size_per_device=1)
+    fn.close()
+
+
+def test_tokenize_fn_padding_layout():
+    cfg = C.tokenizer_config(4096, 1)
+    mp = runner.ReplicatedParams(P.random_params(6, 2), [0])
+    ss = [synthetic.synthetic_protein(n, 7 + n) for n in (52, 60)]
+    fn = OracleTokenizeFn(cfg, [0])
+    out = fn(mp, None, runner.batch_collate([1, 2], ss))
+    assert out["tokens"].shape == (1, 2, 512) and out["tokens"].dtype == np.uint32
+    assert out["n_tokens"].tolist() == [[52, 60]]
+    assert np.all(out["tokens"][0, 0, 52:] == 2730) and np.all(out["tokens"][0, 1, 60:] == 2730)
+    fn.close()
+
+
+def test_shard_for_rank_partitions():
+    items = list(range(11))
+    parts = [runner.shard_for_rank(items, r, 3) for r in range(3)]
+    assert sorted(sum(parts, [])) == items
+    assert all(len(set(a) & set(b)) == 0 for i, a in enumerate(parts) for b in parts[i + 1:])
+    with pytest.raises(ValueError):
+        runner.shard_for_rank(items, 3, 3)

@@ -1,0 +1,53 @@
+"""N>1 path on CPU: two gloo ranks (127.0.0.1), each takes GPU LOCAL_RANK's round-robin shard of
+the PDB list through the CLI; the union of their token files must equal a single-process run."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from pst_amd import params as P
+from pst_amd import pdb, synthetic
+from test_host import OracleTokenizeFn  # noqa: F401  (imported by the worker too)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_two_rank_cli_sharding(tmp_path):
+    import _mr_worker
+    pdb_dir = tmp_path / "pdbs"
+    pdb_dir.mkdir()
+    ss = {f"p{i}": synthetic.synthetic_protein(50 + 3 * i, 70 + i) for i in range(5)}
+    for k, s in ss.items():
+        (pdb_dir / f"{k}.pdb").write_text(pdb.to_pdb_string(s))
+    mdir = tmp_path / "model"
+    mdir.mkdir()
+    P.save_params_npz(str(mdir / "params.npz"), P.random_full_params(6, seed=21))
+    out = tmp_path / "tok"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mr_worker.run, args=(r, 2, port, str(pdb_dir), str(mdir), str(out), q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    shards = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(sum(shards, [])) == sorted(f"{k}.pdb" for k in ss)
+    assert not set(shards[0]) & set(shards[1])
+    assert sorted(os.listdir(out)) == sorted(f"{k}_tokens.npy" for k in ss)
+    from oracle import oracle as O
+    blob = P.pack(P.random_full_params(6, seed=21), 6)
+    for k, s in ss.items():
+        t = np.load(out / f"{k}_tokens.npy")
+        want = O.tokenize(blob, (4,) * 6, 1, s.atom37_positions, s.atom_flags())["tokens"]
+        assert np.array_equal(t[0], want)
