@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--proteins", type=int, default=N_PROT)
     ap.add_argument("--residues", type=int, default=N_RES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=128, help="proteins in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="proteins in the CPU-baseline sample")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_k_mpnn1.json"),
+                    help="PMC-measured HBM bytes per residue of k_mpnn<1> (tools/pmc_traffic.sh)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
 
@@ -115,15 +117,36 @@ def main():
     tk.set_timing(False)
     dom_ms = stage["mpnn1"]
     achieved = MPNN1_ALG_FLOP_PER_RES * residues_per_rank / (dom_ms * 1e-3) / 1e12
+    executed = MPNN1_EXEC_FLOP_PER_RES * residues_per_rank / (dom_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_file):
+        with open(args.traffic_file) as fh:
+            tf = json.load(fh)
+        traffic = {"bytes_per_launch": round((tf["read_bytes_per_residue"] + tf["write_bytes_per_residue"])
+                                             * residues_per_rank),
+                   "read_bytes_per_residue": tf["read_bytes_per_residue"],
+                   "write_bytes_per_residue": tf["write_bytes_per_residue"],
+                   "achieved_GBps": round((tf["read_bytes_per_residue"] + tf["write_bytes_per_residue"])
+                                          * residues_per_rank / (dom_ms * 1e-3) / 1e9, 1),
+                   "source": tf.get("source", args.traffic_file)}
     roofline = {
         "kernel": "k_mpnn<1> (edge MLP L1 + message MLP L2 + node FFN, fused)",
         "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+        "note": "achieved/frac count SURVEY 8d algorithmic FLOPs; the kernel executes "
+                f"{MPNN1_EXEC_FLOP_PER_RES / MPNN1_ALG_FLOP_PER_RES:.3f}x of them (node-projection split, "
+                "DESIGN.md 5): executed_tflops/peak = frac_executed",
         "launch_ms": round(dom_ms, 3),
-        "executed_tflops": round(MPNN1_EXEC_FLOP_PER_RES * residues_per_rank / (dom_ms * 1e-3) / 1e12, 2),
+        "executed_tflops": round(executed, 2),
+        "frac_executed": round(executed / PEAK_FP32_TFLOPS, 4),
         "stage_ms": {k: round(v, 3) for k, v in stage.items()},
         "path_alg_tflops": round(PATH_ALG_FLOP_PER_RES * residues_per_rank / (sum(stage.values()) * 1e-3) / 1e12, 2),
     }
+
+    # PCIe-inclusive rate: host buffers in, host token ids out (pst_tokenize); never `value`
+    t2 = time.perf_counter()
+    tk.tokenize_packed(pos, flags, off)
+    pcie_rate = residues_per_rank / (time.perf_counter() - t2)
 
     cpu = None
     exact = None
@@ -162,6 +185,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "exact_match": exact,
+            "pcie_inclusive_residues_per_s_per_gpu": round(pcie_rate, 1),
         }
         print(json.dumps(out), flush=True)
     tk.close()

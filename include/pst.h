@@ -16,8 +16,8 @@
  *                    stream (what a pipelined runner or bench uses: inputs already in HBM).
  *   pst_aux          the non-token QuantizerOutput fields (quantize, continuous_embedding,
  *                    continuous_embedding_pre_proj; model/quantize.py:183-242).
- *   pst_codebook_aux FSQ distances / soft_proba / argmin over the implicit codebook
- *                    (model/quantize.py:221-239).
+ *   pst_codebook_aux(_device)  FSQ distances / soft_proba / argmin / histogram / perplexity over
+ *                    the implicit codebook (model/quantize.py:205-239).
  *   pst_device_count jax.local_device_count (scripts/inference_runner.py:169-177).
  *   pst_sync / pst_last_error / pst_destroy   runtime plumbing (block_until_ready, errors).
  *
@@ -127,12 +127,27 @@ int pst_tokenize_device(pst_ctx* ctx, const double* d_atom_pos, const uint8_t* d
 int pst_aux(pst_ctx* ctx, float* bounded, float* quantize, float* pre_proj);
 
 /*
- * FSQ aux over the implicit codebook for the LAST call (model/quantize.py:226-239):
- *   distances [T, K]  sum_d (b_d - c_kd)^2, soft_proba [T, K] softmax(distances) (either may be
- *   NULL), argmin [T] uint32 (nearest code; equals the token id except at exact .5 ties).
- * T = number of token rows of the last call (sum of n_tokens_out), host buffers.
+ * FSQ aux over the implicit codebook for the LAST tokenize call (model/quantize.py:205-239),
+ * one row per real token, rows compact in protein order (protein b's token t at row
+ * sum_{b'<b} n_tokens_out[b'] + t):
+ *   distances  [T, K] f32  sum_d (b_d - c_kd)^2   (QuantizerOutput.distances)
+ *   soft_proba [T, K] f32  softmax_k(distances)   (QuantizerOutput.soft_proba, + sign as reference)
+ *   argmin     [T]   u32   nearest code (per-dimension nearest level, lowest on ties)
+ *   histogram  [K]   u32   token-id counts over the T rows (one-hot sum, quantize.py:211-221)
+ *   perplexity [1]   f32   exp(-sum p log(p + 1e-10)), p = histogram / T (quantize.py:222-224)
+ * Host buffers; any pointer may be NULL. `rows` = rows the caller's [T,...] buffers hold
+ * (T = sum of n_tokens_out). Synchronous. K = 64000 → 256 KB per row per tensor.
  */
-int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t* argmin);
+int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t* argmin,
+                     uint32_t* histogram, float* perplexity, int64_t rows);
+
+/*
+ * Same on device buffers, asynchronous on ctx's stream (the kernel is a streaming HBM write of
+ * 4·K bytes per row per tensor). row_capacity must be >= sum_b floor(R_b / df) of the last call
+ * (rows used = sum of n_tokens). The last call's device outputs must still be alive.
+ */
+int pst_codebook_aux_device(pst_ctx* ctx, float* d_distances, float* d_soft_proba,
+                            uint32_t* d_argmin, uint32_t* d_histogram, int64_t row_capacity);
 
 int pst_sync(pst_ctx* ctx);
 

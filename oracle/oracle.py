@@ -35,6 +35,7 @@ def lib():
         L.pst_oracle_encode.argtypes = [P, i, P, i, i, i, P, P, P, P, P, P, P, P, P]
         L.pst_oracle_tokenize.argtypes = [P, i, P, i, i, P, P, i, P, P, P, P]
         L.pst_oracle_tokenize_batch.argtypes = [P, i, P, i, i, P, P, P, i, P, P, i]
+        L.pst_oracle_fsq_aux.argtypes = [P, i, P, ctypes.c_int64, P, P, P]
         for f in ("tanh", "gelu", "exp", "sigmoid"):
             fn = getattr(L, "pst_oracle_" + f)
             fn.restype, fn.argtypes = ctypes.c_float, [ctypes.c_float]
@@ -122,3 +123,24 @@ def tokenize_batch(blob, levels, df, pos, flags, offsets, n_threads=1, k=K):
     if rc != 0:
         raise RuntimeError("oracle batch failed")
     return tok, nt
+
+
+def fsq_aux(levels, bounded):
+    """distances / soft_proba / argmin for rows of continuous embeddings (libpst's canonical
+    formulation, see pst_oracle.c)."""
+    lv = np.asarray(levels, np.int32)
+    b = np.ascontiguousarray(bounded, np.float32).reshape(-1, len(lv))
+    T, K = b.shape[0], int(np.prod(lv))
+    dist = np.zeros((T, K), np.float32)
+    prob = np.zeros((T, K), np.float32)
+    arg = np.zeros(T, np.uint32)
+    if lib().pst_oracle_fsq_aux(_p(lv), len(lv), _p(b), T, _p(dist), _p(prob), _p(arg)) != 0:
+        raise ValueError("fsq_aux needs 4 <= D <= 8")
+    return dict(distances=dist, soft_proba=prob, argmin=arg)
+
+
+def perplexity(tokens, K):
+    """quantize.py:211-224 on the real token rows (f64 accumulation)."""
+    hist = np.bincount(np.asarray(tokens, np.int64), minlength=K).astype(np.float64)
+    p = hist / max(hist.sum(), 1.0)
+    return float(np.exp(-np.sum(p * np.log(p + 1e-10)))), hist.astype(np.uint32)

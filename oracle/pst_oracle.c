@@ -633,3 +633,79 @@ float pst_oracle_gelu(float x) { return c_gelu(x); }
 float pst_oracle_exp(float x) { return c_exp(x); }
 float pst_oracle_sigmoid(float x) { return c_sigmoid(x); }
 double pst_oracle_exp64(double x) { return c_exp64(x); }
+
+/* ------------------------------------------------------------------ FSQ aux (quantize.py:205-239)
+ * Mirrors libpst's k_fsq_aux operation for operation: per row, dims split into a low group
+ * (0..2) and a high group (3..D-1); group tables A/B = sequential sums of (b_d - c)^2; EA/EB =
+ * exp(table - max); group sums in the GPU's order (64 lane partials, each sequential over
+ * i = lane, lane+64, ... from +0, then a xor butterfly 32..1); distance = A + B,
+ * soft_proba = (EA*EB) * (1/(S_A*S_B)); argmin = per-dimension nearest level (lowest on ties). */
+static float group_tables(const float* bv, const int32_t* L, int d0, int d1, float* S, float* E) {
+  int n = 1;
+  for (int d = d0; d < d1; ++d) n *= L[d];
+  float mx = -INFINITY;
+  for (int i = 0; i < n; ++i) {
+    int rem = i;
+    float s = 0.0f;
+    for (int d = d0; d < d1; ++d) {
+      int digit = rem % L[d];
+      rem /= L[d];
+      float diff = bv[d] - (float)(digit - L[d] / 2);
+      float sq = diff * diff;
+      s = d == d0 ? sq : s + sq;
+    }
+    S[i] = s;
+    if (s > mx) mx = s;
+  }
+  float part[64];
+  for (int l = 0; l < 64; ++l) part[l] = 0.0f;
+  for (int i = 0; i < n; ++i) {
+    E[i] = c_exp(S[i] - mx);
+    part[i & 63] = part[i & 63] + E[i];
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    float nx[64];
+    for (int l = 0; l < 64; ++l) nx[l] = part[l] + part[l ^ m];
+    memcpy(part, nx, sizeof(part));
+  }
+  return part[0];
+}
+
+int pst_oracle_fsq_aux(const int32_t* levels, int D, const float* bounded, int64_t T, float* dist,
+                       float* prob, uint32_t* argmin) {
+  if (D < 4 || D > 8) return -1;
+  int K_lo = levels[0] * levels[1] * levels[2], K_hi = 1;
+  for (int d = 3; d < D; ++d) K_hi *= levels[d];
+  int64_t K = (int64_t)K_lo * K_hi;
+  float* A = (float*)malloc(sizeof(float) * K_lo * 2);
+  float* B = (float*)malloc(sizeof(float) * K_hi * 2);
+  for (int64_t r = 0; r < T; ++r) {
+    const float* bv = bounded + r * D;
+    float sa = group_tables(bv, levels, 0, 3, A, A + K_lo);
+    float sb = group_tables(bv, levels, 3, D, B, B + K_hi);
+    float inv_s = 1.0f / (sa * sb);
+    for (int64_t k = 0; k < K; ++k) {
+      int khi = (int)(k / K_lo), klo = (int)(k % K_lo);
+      if (dist) dist[r * K + k] = A[klo] + B[khi];
+      if (prob) prob[r * K + k] = (A[K_lo + klo] * B[K_hi + khi]) * inv_s;
+    }
+    if (argmin) {
+      uint32_t k = 0, basis = 1;
+      for (int d = 0; d < D; ++d) {
+        int best = 0;
+        float bd = INFINITY;
+        for (int g = 0; g < levels[d]; ++g) {
+          float diff = bv[d] - (float)(g - levels[d] / 2);
+          float sq = diff * diff;
+          if (sq < bd) { bd = sq; best = g; }
+        }
+        k += (uint32_t)best * basis;
+        basis *= (uint32_t)levels[d];
+      }
+      argmin[r] = k;
+    }
+  }
+  free(A);
+  free(B);
+  return 0;
+}

@@ -22,6 +22,8 @@ int pst_oracle_tokenize(const float* blob, int D, const int32_t* levels, int df,
 int pst_oracle_tokenize_batch(const float* blob, int D, const int32_t* levels, int df, int k,
                               const double* pos, const uint8_t* flags, const int64_t* offsets,
                               int n_prot, uint32_t* tokens, int32_t* n_tokens, int n_threads);
+int pst_oracle_fsq_aux(const int32_t* levels, int D, const float* bounded, int64_t T, float* dist,
+                       float* prob, uint32_t* argmin);
 float pst_oracle_tanh(float x);
 float pst_oracle_gelu(float x);
 float pst_oracle_exp(float x);

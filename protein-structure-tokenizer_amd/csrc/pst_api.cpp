@@ -211,7 +211,15 @@ struct pst_ctx {
     uint8_t* flags;
     uint32_t* tokens;
     int32_t* n_tok;
+    int64_t* row_start;
   } w{};
+  // last call's outputs the aux kernels read (device; the caller's buffers for pst_tokenize_device)
+  const uint32_t* last_tokens = nullptr;
+  const int32_t* last_nnodes = nullptr;
+  int32_t last_ntiles = 0;
+  // grow-only scratch of pst_codebook_aux (host variant)
+  void* aux = nullptr;
+  size_t aux_bytes = 0;
   std::vector<int64_t> h_offsets;
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
@@ -386,6 +394,7 @@ int ensure_workspace(pst_ctx* ctx, int64_t R, int B) {
       {(void**)&w.bounded, sizeof(float) * 8 * Rpad},   {(void**)&w.quant, sizeof(float) * 8 * Rpad},
       {(void**)&w.pre_proj, sizeof(float) * 128 * Rpad}, {(void**)&w.pos, sizeof(double) * 37 * 3 * Rpad},
       {(void**)&w.flags, sizeof(uint8_t) * 37 * Rpad},  {(void**)&w.tokens, sizeof(uint32_t) * Rpad},
+      {(void**)&w.row_start, sizeof(int64_t) * (B + 1)},
   };
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 4095) / 4096 * 4096;
@@ -553,6 +562,9 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   ctx->last_R = R;
   ctx->last_Rpad = Rpad;
   ctx->last_B = n_prot;
+  ctx->last_tokens = d_tokens;
+  ctx->last_nnodes = d_nnodes;
+  ctx->last_ntiles = (int32_t)tp.size();
   (void)d_ntok;
   return PST_OK;
 }
@@ -659,6 +671,7 @@ int pst_destroy(pst_ctx* ctx) {
     if (ctx->dbg[l]) (void)hipFree(ctx->dbg[l]);
   for (int i = 0; i <= PST_N_STAGES; ++i)
     if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
+  if (ctx->aux) (void)hipFree(ctx->aux);
   for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -736,8 +749,121 @@ int pst_aux(pst_ctx* ctx, float* bounded, float* quantize, float* pre_proj) {
   return PST_OK;
 }
 
-int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t* argmin) {
-  return fail(ctx, PST_E_INVALID, "pst_codebook_aux: not implemented in this build");
+}  // extern "C"
+
+namespace {
+
+// upper bound of the last call's token rows (from the raw residue counts)
+int64_t token_rows_upper(const pst_ctx* ctx) {
+  int64_t t = 0;
+  for (int b = 0; b < ctx->last_B; ++b) t += (ctx->h_offsets[b + 1] - ctx->h_offsets[b]) / ctx->df;
+  return t;
+}
+
+int launch_codebook_aux(pst_ctx* ctx, float* d_dist, float* d_prob, uint32_t* d_argmin, uint32_t* d_hist) {
+  const int D = ctx->D;
+  int K_lo = 1, K_hi = 1;
+  for (int d = 0; d < D; ++d) (d < 3 ? K_lo : K_hi) *= ctx->fsq_L[d];
+  const int K = K_lo * K_hi;
+  if (D < 4 || K_lo > FSQ_AUX_MAX_LO || K_hi > FSQ_AUX_MAX_HI || (K_lo & 3))
+    return fail(ctx, PST_E_INVALID, "codebook aux supports D >= 4, prod(L[0:3]) <= 512 (multiple of 4), "
+                                    "prod(L[3:]) <= 128");
+  pst::FsqAuxArgs a{};
+  a.n_rows_grid = ctx->last_ntiles * 32;
+  a.tile_prot = ctx->w.tile_prot;
+  a.tile_t0 = ctx->w.tile_t0;
+  a.offsets = ctx->w.offsets;
+  a.n_nodes = ctx->last_nnodes;
+  a.row_start = ctx->w.row_start;
+  a.bounded = ctx->w.bounded;
+  a.tokens = ctx->last_tokens;
+  a.df = ctx->df;
+  a.D = D;
+  a.K = K;
+  a.K_lo = K_lo;
+  a.K_hi = K_hi;
+  for (int d = 0; d < 8; ++d) {
+    a.L[d] = d < D ? ctx->fsq_L[d] : 1;
+    a.basis[d] = d < D ? ctx->fsq_basis[d] : 0;
+  }
+  a.dist = d_dist;
+  a.prob = d_prob;
+  a.argmin = d_argmin;
+  a.hist = d_hist;
+  if (d_hist) HIPCHK(hipMemsetAsync(d_hist, 0, sizeof(uint32_t) * K, ctx->stream));
+  pst::launch_fsq_aux(a, ctx->last_B, ctx->stream);
+  HIPCHK(hipGetLastError());
+  return PST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pst_codebook_aux_device(pst_ctx* ctx, float* d_distances, float* d_soft_proba, uint32_t* d_argmin,
+                            uint32_t* d_histogram, int64_t row_capacity) {
+  if (!ctx) return PST_E_INVALID;
+  if (ctx->last_R == 0 || !ctx->last_tokens) return fail(ctx, PST_E_INVALID, "no tokenize call yet");
+  if ((d_distances || d_soft_proba || d_argmin) && row_capacity < token_rows_upper(ctx))
+    return fail(ctx, PST_E_INVALID, "row_capacity below the token-row bound of the last call (sum floor(R_b/df))");
+  HIPCHK(hipSetDevice(ctx->device));
+  return launch_codebook_aux(ctx, d_distances, d_soft_proba, d_argmin, d_histogram);
+}
+
+int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t* argmin, uint32_t* histogram,
+                     float* perplexity, int64_t rows) {
+  if (!ctx) return PST_E_INVALID;
+  if (ctx->last_R == 0 || !ctx->last_tokens) return fail(ctx, PST_E_INVALID, "no tokenize call yet");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int B = ctx->last_B;
+  std::vector<int32_t> nn(B);
+  HIPCHK(hipMemcpyAsync(nn.data(), ctx->last_nnodes, sizeof(int32_t) * B, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  int64_t T = 0;
+  for (int b = 0; b < B; ++b) T += nn[b] / ctx->df;
+  if ((distances || soft_proba || argmin) && rows < T)
+    return fail(ctx, PST_E_INVALID, "output buffers hold " + std::to_string(rows) + " rows, need " + std::to_string(T));
+  int64_t K = 1;
+  for (int d = 0; d < ctx->D; ++d) K *= ctx->fsq_L[d];
+  const size_t tk = (size_t)T * (size_t)K * sizeof(float);
+  auto al = [](size_t x) { return (x + 4095) / 4096 * 4096; };
+  const size_t need = (distances ? al(tk) : 0) + (soft_proba ? al(tk) : 0) + al(sizeof(uint32_t) * (T + 1)) +
+                      al(sizeof(uint32_t) * K);
+  if (need > ctx->aux_bytes) {
+    if (ctx->aux) (void)hipFree(ctx->aux);
+    ctx->aux = nullptr;
+    ctx->aux_bytes = 0;
+    hipError_t e = hipMalloc(&ctx->aux, need);
+    if (e != hipSuccess) return fail(ctx, PST_E_NOMEM, std::string("aux allocation failed: ") + hipGetErrorString(e));
+    ctx->aux_bytes = need;
+  }
+  char* p = (char*)ctx->aux;
+  float* d_dist = distances ? (float*)p : nullptr;
+  p += distances ? al(tk) : 0;
+  float* d_prob = soft_proba ? (float*)p : nullptr;
+  p += soft_proba ? al(tk) : 0;
+  uint32_t* d_arg = (uint32_t*)p;
+  p += al(sizeof(uint32_t) * (T + 1));
+  uint32_t* d_hist = (uint32_t*)p;
+  int rc = launch_codebook_aux(ctx, d_dist, d_prob, argmin ? d_arg : nullptr, d_hist);
+  if (rc) return rc;
+  if (distances && T) HIPCHK(hipMemcpyAsync(distances, d_dist, tk, hipMemcpyDeviceToHost, ctx->stream));
+  if (soft_proba && T) HIPCHK(hipMemcpyAsync(soft_proba, d_prob, tk, hipMemcpyDeviceToHost, ctx->stream));
+  if (argmin && T) HIPCHK(hipMemcpyAsync(argmin, d_arg, sizeof(uint32_t) * T, hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<uint32_t> hist(K);
+  HIPCHK(hipMemcpyAsync(hist.data(), d_hist, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (histogram) std::copy(hist.begin(), hist.end(), histogram);
+  if (perplexity) {  // quantize.py:222-224 (avg_probs = hist / total; exp(-sum p log(p + 1e-10)))
+    double total = 0.0, h = 0.0;
+    for (uint32_t c : hist) total += c;
+    for (uint32_t c : hist) {
+      double pr = total > 0 ? c / total : 0.0;
+      h += pr * std::log(pr + 1e-10);
+    }
+    *perplexity = (float)std::exp(-h);
+  }
+  return PST_OK;
 }
 
 int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes) {

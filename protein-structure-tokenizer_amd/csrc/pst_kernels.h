@@ -115,10 +115,32 @@ struct DownArgs {
   float* pre_proj_out;   // [R,128]
 };
 
+#define FSQ_AUX_MAX_LO 512  // codes of dims 0..2 (8*8*8 for the 64000 codebook)
+#define FSQ_AUX_MAX_HI 128  // codes of dims 3..D-1 (5*5*5)
+
+struct FsqAuxArgs {
+  int32_t n_rows_grid;  // n_tiles * 32 (one workgroup per potential token row)
+  const int32_t* tile_prot;
+  const int32_t* tile_t0;
+  const int64_t* offsets;
+  const int32_t* n_nodes;
+  const int64_t* row_start;  // [B+1] compact output row of each protein's token 0 (k_row_start)
+  const float* bounded;      // [Rpad, 8] continuous_embedding, raw-offset rows
+  const uint32_t* tokens;    // [R] raw-offset token ids
+  int32_t df, D, K, K_lo, K_hi;
+  int32_t L[8];
+  int32_t basis[8];
+  float* dist;         // [T, K] or null
+  float* prob;         // [T, K] or null
+  uint32_t* argmin;    // [T] or null
+  uint32_t* hist;      // [K] (zeroed by the caller) or null
+};
+
 void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st);
 void launch_knn(const KnnArgs& a, hipStream_t st);
 void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st);
 void launch_down(int df, const DownArgs& a, hipStream_t st);
+void launch_fsq_aux(const FsqAuxArgs& a, int n_prot, hipStream_t st);
 void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, float* Y, int ldy,
                        hipStream_t st);
 

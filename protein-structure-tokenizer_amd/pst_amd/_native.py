@@ -34,7 +34,8 @@ class _ModelDesc(ctypes.Structure):
 _lib = None
 EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "pst_create_error",
            "pst_tokenize", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
-           "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing", "pst_device_count")
+           "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing", "pst_device_count",
+           "pst_codebook_aux_device")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -57,7 +58,8 @@ def lib():
         L.pst_tokenize.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
         L.pst_tokenize_device.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
         L.pst_aux.argtypes = [P, P, P, P]
-        L.pst_codebook_aux.argtypes = [P, P, P, P]
+        L.pst_codebook_aux.argtypes = [P, P, P, P, P, P, ctypes.c_int64]
+        L.pst_codebook_aux_device.argtypes = [P, P, P, P, P, ctypes.c_int64]
         L.pst_sync.argtypes = [P]
         L.pst_stream.restype = P
         L.pst_stream.argtypes = [P]
@@ -188,6 +190,22 @@ class Tokenizer:
         pp = np.zeros((R, 128), np.float32)
         self._check(lib().pst_aux(self._h, _ptr(b), _ptr(q), _ptr(pp)))
         return dict(bounded=b, quantize=q, pre_proj=pp)
+
+    def codebook_aux(self, n_rows: int, distances: bool = True, soft_proba: bool = True):
+        """FSQ aux of the last call (pst_codebook_aux): rows compact over real tokens."""
+        K = self.codebook_size
+        dist = np.zeros((n_rows, K), np.float32) if distances else None
+        prob = np.zeros((n_rows, K), np.float32) if soft_proba else None
+        arg = np.zeros(n_rows, np.uint32)
+        hist = np.zeros(K, np.uint32)
+        ppl = np.zeros(1, np.float32)
+        self._check(lib().pst_codebook_aux(self._h, _ptr(dist), _ptr(prob), _ptr(arg), _ptr(hist), _ptr(ppl), n_rows))
+        return dict(distances=dist, soft_proba=prob, argmin=arg, histogram=hist, perplexity=float(ppl[0]))
+
+    def codebook_aux_device(self, d_dist: int, d_prob: int, d_argmin: int, d_hist: int, row_capacity: int):
+        self._check(lib().pst_codebook_aux_device(self._h, ctypes.c_void_p(d_dist or None), ctypes.c_void_p(d_prob or None),
+                                                  ctypes.c_void_p(d_argmin or None), ctypes.c_void_p(d_hist or None),
+                                                  row_capacity))
 
     def debug_fetch(self, which: int, R: int):
         if which in (1, 2, 3):

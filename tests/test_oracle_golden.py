@@ -85,3 +85,18 @@ def test_fsq_index_map_vs_reference():
         idx = ((q + half) * basis).sum(-1)
         assert np.array_equal(idx, np.arange(K))
         assert np.array_equal(G[tag + "/roundtrip"], np.arange(K))
+
+
+def test_fsq_aux_vs_reference():
+    """distances / soft_proba / perplexity (quantize.py:211-239) of the oracle's canonical
+    formulation vs the reference model's own outputs (f64 run, shim) on the same latents."""
+    F = FWD
+    c = "syn51_k4096_df1/"
+    b = F[c + "bounded"].astype(np.float32)
+    a = O.fsq_aux((4,) * 6, b)
+    d, p = F[c + "distances"], F[c + "soft_proba"]
+    np.testing.assert_allclose(a["distances"], d, rtol=1e-6, atol=1e-5)
+    np.testing.assert_allclose(a["soft_proba"], p, rtol=1e-4, atol=1e-6)
+    assert np.array_equal(a["argmin"], F[c + "tokens"])
+    ppl, _ = O.perplexity(F[c + "tokens"], 4096)
+    assert abs(ppl - float(F[c + "perplexity"])) <= 1e-6 * ppl
