@@ -6,6 +6,7 @@ HIP device is missing, loading raises.
 """
 import ctypes
 import os
+import sys
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -39,6 +40,19 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
+def _init_torch_hip_first():
+    """PyTorch-ROCm wheels bundle their own HIP/HSA runtime (libamdhip64.so) next to the system
+    one libpst links (libamdhip64.so.7). Both can serve one process only if torch's runtime
+    opens the GPU first, so when torch is already imported, initialise it before libpst."""
+    torch = sys.modules.get("torch")
+    if torch is not None:
+        try:
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
+
+
 def lib():
     """Load libpst.so (raises if it was not built)."""
     global _lib
@@ -46,6 +60,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise PstError(f"libpst.so not found at {LIB_PATH}: build it with "
                            "`make -C protein-structure-tokenizer_amd/csrc` (no CPU fallback exists)")
+        _init_torch_hip_first()
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         L.pst_param_count.restype = ctypes.c_size_t

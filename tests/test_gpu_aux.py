@@ -2,6 +2,7 @@
 argmin exact, histogram = bincount of the token ids, perplexity per quantize.py:211-224."""
 import numpy as np
 import pytest
+import torch  # before libpst loads: torch's bundled HIP runtime must open the GPU first
 
 from oracle import oracle as O
 from pst_amd import params as P
@@ -41,7 +42,6 @@ def test_codebook_aux_bitwise(cb, df, sizes):
 
 
 def test_codebook_aux_device_matches_host():
-    import torch
     tk, tokens, bounded, T = _run(4096, 2, (100, 256, 57))
     host = tk.codebook_aux(T)
     cap = (100 + 256 + 57) // 2 + 3
