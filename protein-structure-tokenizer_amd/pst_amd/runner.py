@@ -125,9 +125,10 @@ class TokenizeFn:
     the reference's inference path (no stochastic op when is_training=False).
     """
 
-    def __init__(self, cfg: TokenizerConfig, devices: Sequence[int]):
+    def __init__(self, cfg: TokenizerConfig, devices: Sequence[int], emit_aux: bool = False):
         self.cfg = cfg
         self.devices = list(devices)
+        self.emit_aux = emit_aux
         self._ctx: Dict[Tuple[int, int], _native.Tokenizer] = {}
         self._pool = _cf.ThreadPoolExecutor(max_workers=max(1, len(self.devices)))
 
@@ -158,18 +159,73 @@ class TokenizeFn:
             rows = np.full((len(shard), out_len), pad, np.uint32)
             for b in range(len(shard)):
                 rows[b, :nt[b]] = tok[off[b]:off[b] + nt[b]]
-            return rows, nt
+            aux = self._aux(t, shard, off, nt, out_len) if self.emit_aux else None
+            return rows, nt, aux
 
         res = list(self._pool.map(run, range(n_dev)))
-        tokens = np.stack([r for r, _ in res]).reshape(*batched_graph.batch_dims, out_len)
-        n_tokens = np.stack([n for _, n in res]).reshape(*batched_graph.batch_dims)
-        return {"tokens": tokens, "n_tokens": n_tokens}
+        tokens = np.stack([r[0] for r in res]).reshape(*batched_graph.batch_dims, out_len)
+        n_tokens = np.stack([r[1] for r in res]).reshape(*batched_graph.batch_dims)
+        out = {"tokens": tokens, "n_tokens": n_tokens}
+        if self.emit_aux:
+            for key in res[0][2]:
+                if key == "histogram":
+                    continue
+                out[key] = np.stack([r[2][key] for r in res]).reshape(*batched_graph.batch_dims,
+                                                                      *res[0][2][key].shape[1:])
+            # perplexity: mean of the per-device normalised histograms (jax.lax.pmean,
+            # quantize.py:222-224), replicated per device like the reference's output
+            p = np.mean([r[2]["histogram"] / max(r[2]["histogram"].sum(), 1) for r in res], axis=0)
+            ppl = float(np.exp(-np.sum(p * np.log(p + 1e-10))))
+            out["perplexity"] = np.full(n_dev, ppl, np.float32)
+            out["straight_through_quantized"] = out["quantize"]
+        return out
+
+    def _aux(self, t, shard, off, nt, out_len):
+        """Per-shard QuantizerOutput fields, padded to [bpd, out_len, ...] like the reference.
+        Padding rows: quantize / continuous_embedding / distances = 0 (masked, quantize.py:184,
+        236), soft_proba = softmax of the unmasked distances of a zero latent (:235),
+        continuous_embedding_pre_proj = 0 (the reference's value there comes from masked queries
+        and is not consumed)."""
+        D, K = len(self.cfg.levels), t.codebook_size
+        R = int(off[-1])
+        a = t.aux(R)
+        T = int(nt.sum())
+        ca = t.codebook_aux(T)
+        bpd = len(shard)
+        o = {"quantize": np.zeros((bpd, out_len, D), np.float32),
+             "continuous_embedding": np.zeros((bpd, out_len, D), np.float32),
+             "continuous_embedding_pre_proj": np.zeros((bpd, out_len, 128), np.float32),
+             "distances": np.zeros((bpd, out_len, K), np.float32),
+             "soft_proba": np.broadcast_to(_padded_soft_proba(self.cfg.levels), (bpd, out_len, K)).copy()}
+        r0 = 0
+        for b in range(bpd):
+            n = int(nt[b])
+            src = slice(int(off[b]), int(off[b]) + n)
+            o["quantize"][b, :n] = a["quantize"][src]
+            o["continuous_embedding"][b, :n] = a["bounded"][src]
+            o["continuous_embedding_pre_proj"][b, :n] = a["pre_proj"][src]
+            o["distances"][b, :n] = ca["distances"][r0:r0 + n]
+            o["soft_proba"][b, :n] = ca["soft_proba"][r0:r0 + n]
+            r0 += n
+        o["histogram"] = ca["histogram"].astype(np.float64)
+        return o
 
     def close(self):
         for t in self._ctx.values():
             t.close()
         self._ctx.clear()
         self._pool.shutdown(wait=True)
+
+
+def _padded_soft_proba(levels: Sequence[int]) -> np.ndarray:
+    """softmax_k(sum_d c_kd^2): soft_proba of a masked row (its latent is 0)."""
+    lv = np.asarray(levels)
+    basis = np.concatenate(([1], np.cumprod(lv[:-1])))
+    k = np.arange(int(np.prod(lv)))[:, None]
+    c = (k // basis) % lv - lv // 2
+    d = np.sum(c.astype(np.float32) ** 2, axis=-1)
+    e = np.exp(d - d.max())
+    return (e / e.sum()).astype(np.float32)
 
 
 # ------------------------------------------------------------------------------------- runner
@@ -193,8 +249,11 @@ class InferenceRunner:
         return list(range(n)), n
 
     @staticmethod
-    def prepare_tokenize_fn(cfg: TokenizerConfig, devices: Sequence[int]) -> Callable:
-        return TokenizeFn(cfg, devices)
+    def prepare_tokenize_fn(cfg: TokenizerConfig, devices: Sequence[int], emit_aux: bool = False) -> Callable:
+        """`emit_aux=True` also returns the other QuantizerOutput fields (quantize,
+        straight_through_quantized, continuous_embedding, continuous_embedding_pre_proj,
+        distances, soft_proba, perplexity) shaped [n_dev, bpd, seq_max/df, ...] as the reference."""
+        return TokenizeFn(cfg, devices, emit_aux)
 
     @staticmethod
     def load_params(model_dir: str, local_devices: Sequence[int]) -> ReplicatedParams:

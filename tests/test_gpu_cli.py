@@ -54,3 +54,32 @@ def test_tokenize_fn_on_gpu_matches_reference_layout():
         want = O.tokenize(mp.blob, cfg.levels, 1, s.atom37_positions, s.atom_flags())["tokens"]
         assert np.array_equal(out["tokens"][0, b, :s.nb_residues], want)
         assert np.all(out["tokens"][0, b, s.nb_residues:] == runner.pad_token_value(cfg.levels))
+
+
+def test_tokenize_fn_emit_aux_matches_reference_golden():
+    """QuantizerOutput through the runner mirror vs the reference model's own outputs (f64 run
+    under the shim, same random weights): tokens exact, aux within f32 tolerance."""
+    F = np.load(os.path.join(os.path.dirname(__file__), "golden", "forward_golden_f64.npz"))
+    c = "syn51_k4096_df1/"
+    from pst_amd.sample import ProteinStructureSample
+    pos = F[c + "in_positions"].astype(np.float64)
+    fl = F[c + "in_flags"]
+    n = pos.shape[0]
+    s = ProteinStructureSample(None, n, np.zeros((n, 21)), pos, (fl & 1).astype(bool), ((fl >> 1) & 1).astype(bool), 0.0, 1)
+    cfg = C.tokenizer_config(4096, 1)
+    mp = runner.ReplicatedParams(P.random_params(6, 1234), [0])
+    fn = runner.InferenceRunner.prepare_tokenize_fn(cfg, [0], emit_aux=True)
+    out = fn(mp, None, runner.batch_collate([1, 1], [s]))
+    fn.close()
+    T = int(out["n_tokens"][0, 0])
+    assert T == F[c + "tokens"].shape[0]
+    assert np.array_equal(out["tokens"][0, 0, :T], F[c + "tokens"])
+    np.testing.assert_allclose(out["continuous_embedding"][0, 0, :T], F[c + "bounded"], atol=1e-4)
+    np.testing.assert_allclose(out["continuous_embedding_pre_proj"][0, 0, :T], F[c + "pre_proj"], atol=5e-6)
+    np.testing.assert_array_equal(out["quantize"][0, 0, :T], F[c + "quantize"])
+    np.testing.assert_array_equal(out["straight_through_quantized"], out["quantize"])
+    np.testing.assert_allclose(out["distances"][0, 0, :T], F[c + "distances"], rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(out["soft_proba"][0, 0, :T], F[c + "soft_proba"], rtol=1e-3, atol=1e-5)
+    assert abs(out["perplexity"][0] - float(F[c + "perplexity"])) < 1e-4 * float(F[c + "perplexity"])
+    assert np.all(out["distances"][0, 0, T:] == 0) and np.all(out["quantize"][0, 0, T:] == 0)
+    np.testing.assert_allclose(out["soft_proba"][0, 0, T:].sum(-1), 1.0, rtol=1e-5)
