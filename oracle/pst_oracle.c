@@ -57,11 +57,31 @@ static float c_tanh(float a) {
   return fabsf(a) < 0.0004f ? a : r;
 }
 
+/* tanh's rational core without the |x| < 4e-4 shortcut (used inside GELU) */
+static float c_tanh_core(float a) {
+  const float clamp = 7.99881172180175781f;
+  float x = a > clamp ? clamp : (a < -clamp ? -clamp : a);
+  float x2 = x * x;
+  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = fmaf(x2, p, -8.60467152213735e-11f);
+  p = fmaf(x2, p, 5.12229709037114e-08f);
+  p = fmaf(x2, p, 1.48572235717979e-05f);
+  p = fmaf(x2, p, 6.37261928875436e-04f);
+  p = fmaf(x2, p, 4.89352455891786e-03f);
+  p = x * p;
+  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = fmaf(x2, q, 2.26843463243900e-03f);
+  q = fmaf(x2, q, 4.89352518554385e-03f);
+  return p / q;
+}
+
+/* GELU (tanh form, jax.nn.gelu approximate=True) in the canonical GPU-friendly sequence:
+ * u = x * (k0 + k0k1 x^2), g = h + h * tanh(u), h = x/2. Within 2 ulp of
+ * x * 0.5 * (1 + tanh(k0 (x + k1 x^3))). */
 static float c_gelu(float x) {
-  float x3 = x * (x * x);
-  float inner = 0.797884583473205566f * (x + 0.0447149984538555145f * x3);
-  float cdf = 0.5f * (1.0f + c_tanh(inner));
-  return x * cdf;
+  float u = x * fmaf(x * x, 0.035677406936883926f, 0.797884583473205566f);
+  float hx = 0.5f * x;
+  return fmaf(hx, c_tanh_core(u), hx);
 }
 
 static float c_ldexpf(float v, int n) {
@@ -398,21 +418,23 @@ typedef struct {
   const float* feat;      /* [n*k*32] */
 } graph_t;
 
+/* Every Linear's fma chain starts from its bias ("bias-first"); the first layer of an edge
+ * MLP starts from Ps[s] + Pr[r], where Pr's own chain started from that layer's bias. */
 static void mlp3(const float* Ps, const float* Pr, const float* e, const lin_t* L, int act_last, float* y) {
   float init[H], t1[H], t2[H];
   for (int c = 0; c < H; ++c) init[c] = Ps[c] + Pr[c];
-  gemv(e, H, L[0].w + 2 * H * H, H, H, init, L[0].b, t1);
+  gemv(e, H, L[0].w + 2 * H * H, H, H, init, NULL, t1);
   for (int c = 0; c < H; ++c) t1[c] = c_gelu(t1[c]);
-  gemv(t1, H, L[1].w, H, H, NULL, L[1].b, t2);
+  gemv(t1, H, L[1].w, H, H, L[1].b, NULL, t2);
   for (int c = 0; c < H; ++c) t2[c] = c_gelu(t2[c]);
-  gemv(t2, H, L[2].w, H, H, NULL, L[2].b, y);
+  gemv(t2, H, L[2].w, H, H, L[2].b, NULL, y);
   (void)act_last;
 }
 
-/* node projections of an MLP's first layer: Ps = h W[0:128], Pr = h W[128:256] (no bias) */
+/* node projections of an MLP's first layer: Ps = h W[0:128] (from 0), Pr = b + h W[128:256] */
 static void proj2(const float* h, const lin_t* L0, float* Ps, float* Pr) {
   gemv(h, H, L0->w, H, H, NULL, NULL, Ps);
-  gemv(h, H, L0->w + H * H, H, H, NULL, NULL, Pr);
+  gemv(h, H, L0->w + H * H, H, H, L0->b, NULL, Pr);
 }
 
 int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, int n, int k,
@@ -443,7 +465,7 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
   float* Ttab = (float*)malloc(sizeof(float) * 1023 * H);
   for (int x = -511; x <= 511; ++x) {
     pst_oracle_pe_row(x, 512, pe);
-    gemv(pe, H, P.edge_embed.w, H, H, NULL, NULL, Ttab + (size_t)(x + 511) * H);
+    gemv(pe, H, P.edge_embed.w, H, H, P.edge_embed.b, NULL, Ttab + (size_t)(x + 511) * H);
   }
   float* Wf = (float*)calloc(32 * H, sizeof(float));
   memcpy(Wf, P.edge_embed.w + H * H, sizeof(float) * 27 * H);
@@ -454,7 +476,7 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
       float f32[32];
       memcpy(f32, feat + slot * 32, sizeof(f32));
       for (int c = 27; c < 32; ++c) f32[c] = 0.0f;
-      gemv(f32, 32, Wf, H, H, Ttab + (size_t)(s - r + 511) * H, P.edge_embed.b, e + slot * H);
+      gemv(f32, 32, Wf, H, H, Ttab + (size_t)(s - r + 511) * H, NULL, e + slot * H);
     }
   free(Ttab);
   free(Wf);
@@ -486,9 +508,9 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
       }
       for (int c = 0; c < H; ++c) x[c] = h[(size_t)r * H + c] + agg[c] / 50.0f;
       layer_norm(x, M->ln_s[0], M->ln_o[0], h1);
-      gemv(h1, H, M->ff[0].w, 4 * H, 4 * H, NULL, M->ff[0].b, f1);
+      gemv(h1, H, M->ff[0].w, 4 * H, 4 * H, M->ff[0].b, NULL, f1);
       for (int c = 0; c < 4 * H; ++c) f1[c] = c_gelu(f1[c]);
-      gemv(f1, 4 * H, M->ff[1].w, H, H, NULL, M->ff[1].b, f2);
+      gemv(f1, 4 * H, M->ff[1].w, H, H, M->ff[1].b, NULL, f2);
       for (int c = 0; c < H; ++c) x[c] = h1[c] + f2[c];
       layer_norm(x, M->ln_s[1], M->ln_o[1], hn + (size_t)r * H);
     }

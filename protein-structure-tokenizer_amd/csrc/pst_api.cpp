@@ -121,6 +121,15 @@ std::vector<float> frag_narrow(const float* W, int ldw, int O) {  // K = 128, ou
   return f;
 }
 
+// bias fragment for tile_gemm_bf: [64 lanes] float4, lane l < 32 holds b[32M + l] in
+// component M, lanes 32..63 zeros
+std::vector<float> bfrag(const float* b) {
+  std::vector<float> f(64 * 4, 0.0f);
+  for (int lane = 0; lane < 32; ++lane)
+    for (int M = 0; M < 4; ++M) f[lane * 4 + M] = b[32 * M + lane];
+  return f;
+}
+
 std::vector<float> perm(const float* v) {  // 128-vector → perm order
   std::vector<float> p(128);
   for (int h = 0; h < 2; ++h)
@@ -161,11 +170,11 @@ std::vector<float> pe_rows(int x0, int count, int n) {
 }
 
 struct MlpOff {
-  size_t w0, b0, w1, b1, w2, b2;
+  size_t w0, b0, w1, b1, w2, b2, bf0, bf1, bf2;
 };
 struct LayerOff {
   MlpOff msg, edge;
-  size_t ff_w1, ff_b1, ff_w2, ff_b2, proj;  // proj: filled per kernel
+  size_t ff_w1, ff_b1, ff_w2, ff_b2, ff_bf1, ff_bf2, proj;  // proj: filled per kernel
   size_t ln_s[3], ln_o[3];
 };
 struct BlockOff {
@@ -264,11 +273,16 @@ int build_weights(pst_ctx* ctx, const float* blob) {
       o.b1 = A.add(perm(m[1].b));
       o.w2 = A.add(frag(m[2].w, H, 0, 128, 128, 0, 128));
       o.b2 = A.add(perm(m[2].b));
+      o.bf0 = A.add(bfrag(m[0].b));
+      o.bf1 = A.add(bfrag(m[1].b));
+      o.bf2 = A.add(bfrag(m[2].b));
     };
     mlp(S.msg, O.msg);
     mlp(S.edge, O.edge);
-    std::vector<float> w1, b1, w2;
+    std::vector<float> w1, b1, w2, bf1;
     for (int ck = 0; ck < 4; ++ck) {
+      auto bfr = bfrag(S.ff[0].b + 128 * ck);
+      bf1.insert(bf1.end(), bfr.begin(), bfr.end());
       auto f = frag(S.ff[0].w, 4 * H, 0, 128, 128, 128 * ck, 128);
       w1.insert(w1.end(), f.begin(), f.end());
       auto bp = perm(S.ff[0].b + 128 * ck);
@@ -280,13 +294,16 @@ int build_weights(pst_ctx* ctx, const float* blob) {
     O.ff_b1 = A.add(b1);
     O.ff_w2 = A.add(w2);
     O.ff_b2 = A.add(perm(S.ff[1].b));
+    O.ff_bf1 = A.add(bf1);
+    O.ff_bf2 = A.add(bfrag(S.ff[1].b));
     for (int i = 0; i < 3; ++i) {
       O.ln_s[i] = A.add(perm(S.ln_s[i]));
       O.ln_o[i] = A.add(perm(S.ln_o[i]));
     }
   }
   // projections produced by kernel l for kernel l+1: [E_s, E_r] (edge MLP of layer l),
-  // [M_s, M_r] (message MLP of layer l+1): first-layer rows 0..127 / 128..255, no bias
+  // [M_s, M_r] (message MLP of layer l+1): first-layer rows 0..127 / 128..255; the receiver
+  // parts chain from the first-layer bias (k_mpnn node phase)
   for (int l = 0; l < 2; ++l) {
     const Layer& S = P.L[l];
     const Layer& N = P.L[l + 1];
@@ -344,10 +361,12 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   HIPCHK(hipMemcpy(ctx->d_RPE, rpe.data(), rpe.size() * sizeof(float), hipMemcpyHostToDevice));
   float* a = ctx->d_arena;
   auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(a + o); };
-  pst::launch_table_gemm(a + o_npe, 512, F4(o_ne_w), a + o_ne_b, ctx->d_h0, 128, ctx->stream);
-  pst::launch_table_gemm(ctx->d_h0, 512, F4(o_m0s), nullptr, ctx->d_PM0, 256, ctx->stream);
-  pst::launch_table_gemm(ctx->d_h0, 512, F4(o_m0r), nullptr, ctx->d_PM0 + 128, 256, ctx->stream);
-  pst::launch_table_gemm(a + o_epe, 1023, F4(o_ee_w), nullptr, ctx->d_T, 128, ctx->stream);
+  // h0 = nodePE·W + b; PM0 = [h0·W0[0:128] | b0 + h0·W0[128:256]] (message MLP of layer 0);
+  // T = b + edgePE·W[0:128] (the edge embedding's bias is folded into its table)
+  pst::launch_table_gemm(a + o_npe, 512, F4(o_ne_w), a + o_ne_b, nullptr, ctx->d_h0, 128, ctx->stream);
+  pst::launch_table_gemm(ctx->d_h0, 512, F4(o_m0s), nullptr, nullptr, ctx->d_PM0, 256, ctx->stream);
+  pst::launch_table_gemm(ctx->d_h0, 512, F4(o_m0r), nullptr, a + ctx->L[0].msg.b0, ctx->d_PM0 + 128, 256, ctx->stream);
+  pst::launch_table_gemm(a + o_epe, 1023, F4(o_ee_w), nullptr, a + ctx->emb_b, ctx->d_T, 128, ctx->stream);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(ctx->stream));
   // FSQ constants (quantize.py:175-181, computed in float32 as JAX does)
@@ -475,7 +494,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   const float* A = ctx->d_arena;
   auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(A + o); };
   auto mlp = [&](const MlpOff& o) {
-    return pst::MlpW{F4(o.w0), A + o.b0, F4(o.w1), A + o.b1, F4(o.w2), A + o.b2};
+    return pst::MlpW{F4(o.w0), A + o.b0, F4(o.w1), A + o.b1, F4(o.w2), A + o.b2, F4(o.bf1), F4(o.bf2)};
   };
   float* hbuf[4] = {nullptr, w.h0, w.h1, w.h0};
   float* ebuf[3] = {w.e0, w.e1, nullptr};
@@ -512,6 +531,12 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.ff_w2 = F4(L.ff_w2);
     m.ff_b2 = A + L.ff_b2;
     m.proj_w = l < 2 ? F4(ctx->proj[l]) : nullptr;
+    if (l < 2) {
+      m.proj_bf[0] = F4(ctx->L[l].edge.bf0);     // E_r: edge MLP of layer l
+      m.proj_bf[1] = F4(ctx->L[l + 1].msg.bf0);  // M_r: message MLP of layer l+1
+    }
+    m.ff_bf1 = F4(L.ff_bf1);
+    m.ff_bf2 = F4(L.ff_bf2);
     m.e_out = ebuf[l];
     m.h_out = hbuf[l + 1];
     m.P_out = pbuf[l];

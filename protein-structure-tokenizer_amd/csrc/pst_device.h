@@ -47,51 +47,63 @@ __device__ __forceinline__ float c_tanh(float a) {
   return fabsf(a) < 0.0004f ? a : r;
 }
 
+// tanh's rational core without the |x| < 4e-4 shortcut (used inside GELU)
+__device__ __forceinline__ float c_tanh_core(float a) {
+  const float clamp = 7.99881172180175781f;
+  float x = fminf(fmaxf(a, -clamp), clamp);
+  float x2 = x * x;
+  float p = __builtin_fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = __builtin_fmaf(x2, p, -8.60467152213735e-11f);
+  p = __builtin_fmaf(x2, p, 5.12229709037114e-08f);
+  p = __builtin_fmaf(x2, p, 1.48572235717979e-05f);
+  p = __builtin_fmaf(x2, p, 6.37261928875436e-04f);
+  p = __builtin_fmaf(x2, p, 4.89352455891786e-03f);
+  p = x * p;
+  float q = __builtin_fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = __builtin_fmaf(x2, q, 2.26843463243900e-03f);
+  q = __builtin_fmaf(x2, q, 4.89352518554385e-03f);
+  return div_tanh(p, q);
+}
+
+// GELU (tanh form), canonical sequence: u = x (k0 + k0k1 x^2),
+// g = h + h tanh(u), h = x / 2
+#define GELU_K0 0.797884583473205566f
+#define GELU_K0K1 0.035677406936883926f
 __device__ __forceinline__ float c_gelu(float x) {
-  float x3 = x * (x * x);
-  float inner = 0.797884583473205566f * (x + 0.0447149984538555145f * x3);
-  float cdf = 0.5f * (1.0f + c_tanh(inner));
-  return x * cdf;
+  float u = x * __builtin_fmaf(x * x, GELU_K0K1, GELU_K0);
+  float hx = 0.5f * x;
+  return __builtin_fmaf(hx, c_tanh_core(u), hx);
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 splat2(float v) { return (f32x2){v, v}; }
 
-// Two c_gelu evaluations with packed f32 math (v_pk_fma/mul/add_f32): bit-identical to c_gelu
-// on each element, about half the VALU issue cycles.
+// Two c_gelu evaluations with packed f32 math (v_pk_fma/mul_f32): bit-identical to c_gelu on
+// each element, about half the VALU issue cycles.
 __device__ __forceinline__ f32x2 c_gelu2(f32x2 x) {
-  const f32x2 clampv = {7.99881172180175781f, 7.99881172180175781f};
-  f32x2 x2_ = x * x;
-  f32x2 x3 = x * x2_;
-  f32x2 inner = (f32x2){0.797884583473205566f, 0.797884583473205566f} *
-                (x + (f32x2){0.0447149984538555145f, 0.0447149984538555145f} * x3);
-  f32x2 a = inner;
-  f32x2 xc = __builtin_elementwise_min(__builtin_elementwise_max(a, -clampv), clampv);
+  f32x2 u = x * pk_fma(x * x, splat2(GELU_K0K1), splat2(GELU_K0));
+  const f32x2 clampv = splat2(7.99881172180175781f);
+  f32x2 xc = __builtin_elementwise_min(__builtin_elementwise_max(u, -clampv), clampv);
   f32x2 s = xc * xc;
-  f32x2 p = pk_fma(s, (f32x2){-2.76076847742355e-16f, -2.76076847742355e-16f},
-                   (f32x2){2.00018790482477e-13f, 2.00018790482477e-13f});
-  p = pk_fma(s, p, (f32x2){-8.60467152213735e-11f, -8.60467152213735e-11f});
-  p = pk_fma(s, p, (f32x2){5.12229709037114e-08f, 5.12229709037114e-08f});
-  p = pk_fma(s, p, (f32x2){1.48572235717979e-05f, 1.48572235717979e-05f});
-  p = pk_fma(s, p, (f32x2){6.37261928875436e-04f, 6.37261928875436e-04f});
-  p = pk_fma(s, p, (f32x2){4.89352455891786e-03f, 4.89352455891786e-03f});
+  f32x2 p = pk_fma(s, splat2(-2.76076847742355e-16f), splat2(2.00018790482477e-13f));
+  p = pk_fma(s, p, splat2(-8.60467152213735e-11f));
+  p = pk_fma(s, p, splat2(5.12229709037114e-08f));
+  p = pk_fma(s, p, splat2(1.48572235717979e-05f));
+  p = pk_fma(s, p, splat2(6.37261928875436e-04f));
+  p = pk_fma(s, p, splat2(4.89352455891786e-03f));
   p = xc * p;
-  f32x2 q = pk_fma(s, (f32x2){1.19825839466702e-06f, 1.19825839466702e-06f},
-                   (f32x2){1.18534705686654e-04f, 1.18534705686654e-04f});
-  q = pk_fma(s, q, (f32x2){2.26843463243900e-03f, 2.26843463243900e-03f});
-  q = pk_fma(s, q, (f32x2){4.89352518554385e-03f, 4.89352518554385e-03f});
+  f32x2 q = pk_fma(s, splat2(1.19825839466702e-06f), splat2(1.18534705686654e-04f));
+  q = pk_fma(s, q, splat2(2.26843463243900e-03f));
+  q = pk_fma(s, q, splat2(4.89352518554385e-03f));
   // division core (see div_tanh), packed
   f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
-  const f32x2 one = {1.0f, 1.0f};
   f32x2 y = p * r;
   f32x2 e = pk_fma(-q, y, p);
-  y = pk_fma(e, r, y);
-  f32x2 t;
-  t.x = fabsf(a.x) < 0.0004f ? a.x : y.x;
-  t.y = fabsf(a.y) < 0.0004f ? a.y : y.y;
-  f32x2 cdf = (f32x2){0.5f, 0.5f} * (one + t);
-  return x * cdf;
+  f32x2 t = pk_fma(e, r, y);
+  f32x2 hx = splat2(0.5f) * x;
+  return pk_fma(hx, t, hx);
 }
 
 __device__ __forceinline__ float c_ldexpf(float v, int n) {
@@ -291,18 +303,32 @@ __device__ __forceinline__ void tile_gemm_f(Tile& acc, const Tile& X, const floa
   }
 }
 
+// acc = bias + X·W: the bias enters as an extra leading k-step (A = bias fragment, lane half 0
+// holds b[32M + (lane&31)], half 1 zeros; B = 1 on half 0, 0 on half 1), so the chain starts
+// from exactly b without a VALU add or a 64-register bias tile.
+template <typename F>
+__device__ __forceinline__ void tile_gemm_bf(Tile& acc, const Tile& X, const float4* __restrict__ Wf,
+                                             const float4* __restrict__ Bf, F&& f) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Bf);
+  const float4 bb = buf_load4(rs, lane_id() * 16, 0);
+  const float one = lane_id() < 32 ? 1.0f : 0.0f;
+  const f32x16 z = {};
+  acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.x, one, z, 0, 0, 0);
+  acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.y, one, z, 0, 0, 0);
+  acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.z, one, z, 0, 0, 0);
+  acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.w, one, z, 0, 0, 0);
+  tile_gemm_f(acc, X, Wf, f);
+}
+
 // Activation functors: f(t, {x_t, x_t+1}) -> B operands of k-steps t, t+1.
 struct ActId {
   __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return x; }
 };
 
-// bias (perm-ordered vector, this lane's half) + GELU
-struct ActBiasGelu {
-  const float* b;
-  __device__ __forceinline__ f32x2 operator()(int t, f32x2 x) const {
-    const float* bb = b + (lane_id() >> 5) * 64 + t;
-    return c_gelu2(x + (f32x2){bb[0], bb[1]});
-  }
+// GELU of the previous layer's output (its bias is already in the accumulator: chains start
+// from the bias)
+struct ActGelu {
+  __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return c_gelu2(x); }
 };
 
 struct ActBiasRelu {

@@ -38,6 +38,8 @@ struct MlpW {  // one 3-layer MLP on the edge tile; w*: A fragments [64][64] flo
   const float* b1;
   const float4* w2;
   const float* b2;
+  const float4* bf1;  // bias fragments [64 lanes] float4 (see tile_gemm_bf)
+  const float4* bf2;
 };
 
 struct MpnnArgs {
@@ -49,7 +51,7 @@ struct MpnnArgs {
   const float* feat;       // graph edge features
   const float* Ttab;       // [1023][128] perm: edge PE projection
   const float4* W_embed;   // [16][64] float4: init_edge_embed rows 128..154 (+zero pad)
-  const float* b_embed;    // perm
+  const float* b_embed;    // perm (folded into Ttab: unused by the kernel)
   const float* PM0;        // [512][256] perm: h0 · msg0 W[0:128] | W[128:256]
   const float* h0tab;      // [512][128] perm: init_node_embed(node PE)
   // layers >= 1
@@ -70,6 +72,9 @@ struct MpnnArgs {
   const float4* ff_w2;  // [4 chunks][64][64]
   const float* ff_b2;
   const float4* proj_w;  // [4][64][64]: next kernel's E_s, E_r, M_s, M_r projections (or null)
+  const float4* proj_bf[2];  // bias fragments: first-layer biases the E_r / M_r chains start from
+  const float4* ff_bf1;      // [4 chunks][64 lanes] float4 bias fragments
+  const float4* ff_bf2;
   float* agg;  // [n_tasks][32][128] scratch: segment sums (perm order)
   // outputs
   float* e_out;  // blocked (null for the last layer)
@@ -141,7 +146,8 @@ void launch_knn(const KnnArgs& a, hipStream_t st);
 void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st);
 void launch_down(int df, const DownArgs& a, hipStream_t st);
 void launch_fsq_aux(const FsqAuxArgs& a, int n_prot, hipStream_t st);
-void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, float* Y, int ldy,
-                       hipStream_t st);
+// Y = (init or 0) + X·W (+ b): init / b perm-ordered 128-vectors (either may be null)
+void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, const float* init, float* Y,
+                       int ldy, hipStream_t st);
 
 }  // namespace pst

@@ -260,16 +260,14 @@ __device__ __forceinline__ void tile_add_rows(Tile& acc, const float* __restrict
   tile_add(acc, t);
 }
 
-// 3-layer edge MLP starting from acc = init (already Ps + Pr): acc <- MLP(init, X).
-// Bias + GELU of layers 1 and 2 are applied just in time inside the next GEMM.
+// 3-layer edge MLP starting from acc = init (Ps[s] + Pr[r], Pr's chain started from b0):
+// acc <- MLP(init, X). Layers 2 and 3 chain from their biases; the GELU of layers 1 and 2 is
+// applied just in time inside the next GEMM.
 __device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
   tile_gemm(acc, X, W.w0);
   Tile a2;
-  tile_zero(a2);
-  tile_gemm_f(a2, acc, W.w1, ActBiasGelu{W.b0});
-  tile_zero(acc);
-  tile_gemm_f(acc, a2, W.w2, ActBiasGelu{W.b1});
-  tile_add_vec(acc, W.b2);
+  tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu{});
+  tile_gemm_bf(acc, a2, W.w2, W.bf2, ActGelu{});
 }
 
 template <int LAYER>
@@ -302,7 +300,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 #endif
     Tile e;
     if (LAYER == 0) {
-      // init_edge_embed: chain from T[s-r] over the 27 (+5 zero) features, + bias
+      // init_edge_embed: chain from T[s-r] (= b + edgePE(s-r) W[0:128]) over the 27 (+5 zero) features
       int lr = a.node_local[g], ls = a.node_local[s];
       lr = lr < 0 ? 0 : lr;
       ls = ls < 0 ? lr : ls;
@@ -323,7 +321,6 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
         e.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, x[r], e.m[2], 0, 0, 0);
         e.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, x[r], e.m[3], 0, 0, 0);
       }
-      tile_add_vec(e, a.b_embed);
     } else {
       // edge update of layer LAYER-1: e = LN(e + MLP([h_s | h_r | e]))
       Tile ein;
@@ -417,14 +414,14 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   }
   tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0
   Tile out;
-  tile_zero(out);
   for (int ck = 0; ck < 4; ++ck) {
     Tile hid;
-    tile_zero(hid);
-    tile_gemm(hid, x, a.ff_w1 + ck * 64 * 64);
-    tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActBiasGelu{a.ff_b1 + ck * 128});
+    tile_gemm_bf(hid, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, ActId{});
+    if (ck == 0)
+      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu{});
+    else
+      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu{});
   }
-  tile_add_vec(out, a.ff_b2);
   tile_add(x, out);
   tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
   tile_store_perm(x, a.h_out + gl * 128);
@@ -432,8 +429,12 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 #pragma unroll 1
     for (int p = 0; p < 4; ++p) {
       Tile pr;
-      tile_zero(pr);
-      tile_gemm(pr, x, a.proj_w + p * 64 * 64);
+      if (p & 1) {  // receiver parts chain from the layer's first-layer bias
+        tile_gemm_bf(pr, x, a.proj_w + p * 64 * 64, a.proj_bf[p >> 1], ActId{});
+      } else {
+        tile_zero(pr);
+        tile_gemm(pr, x, a.proj_w + p * 64 * 64);
+      }
       tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
     }
   }
@@ -644,7 +645,7 @@ __global__ __launch_bounds__(256) void k_down(DownArgs a) {
 // Y[row] = X[row] · W (+ b); rows of X and Y in perm order, 32 rows per wave.
 __global__ __launch_bounds__(256) void k_table_gemm(const float* __restrict__ X, int n_rows,
                                                     const float4* __restrict__ Wf, const float* __restrict__ b,
-                                                    float* __restrict__ Y, int ldy) {
+                                                    const float* __restrict__ init, float* __restrict__ Y, int ldy) {
   const int lane = threadIdx.x & 63;
   const int wtile = blockIdx.x * 4 + (threadIdx.x >> 6);
   int row = wtile * 32 + (lane & 31);
@@ -652,7 +653,10 @@ __global__ __launch_bounds__(256) void k_table_gemm(const float* __restrict__ X,
   int rc = row < n_rows ? row : n_rows - 1;
   Tile x, acc;
   tile_load_perm(x, X + (int64_t)rc * 128);
-  tile_zero(acc);
+  if (init)
+    tile_load_perm(acc, init);
+  else
+    tile_zero(acc);
   tile_gemm(acc, x, Wf);
   if (b) tile_add_vec(acc, b);
   if (row < n_rows) tile_store_perm(acc, Y + (int64_t)row * ldy);
@@ -677,10 +681,10 @@ void launch_down(int df, const DownArgs& a, hipStream_t st) {
   else if (df == 2) hipLaunchKernelGGL(k_down<2>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(k_down<4>, grid, dim3(256), 0, st, a);
 }
-void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, float* Y, int ldy,
-                       hipStream_t st) {
+void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, const float* init, float* Y,
+                       int ldy, hipStream_t st) {
   int tiles = (n_rows + 31) / 32;
-  hipLaunchKernelGGL(k_table_gemm, dim3((tiles + 3) / 4), dim3(256), 0, st, X, n_rows, Wf, b, Y, ldy);
+  hipLaunchKernelGGL(k_table_gemm, dim3((tiles + 3) / 4), dim3(256), 0, st, X, n_rows, Wf, b, init, Y, ldy);
 }
 
 }  // namespace pst
