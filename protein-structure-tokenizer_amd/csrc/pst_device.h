@@ -193,10 +193,16 @@ __device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t rs, int voff,
 __device__ __forceinline__ float buf_load1(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
 }
+#ifndef PST_E_STORE_AUX
+#define PST_E_STORE_AUX 0
+#endif
+#ifndef PST_E_LOAD_AUX
+#define PST_E_LOAD_AUX 0
+#endif
 __device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t rs, int voff, int soff, float a, float b, float c,
                                            float d) {
   u32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, PST_E_STORE_AUX);
 }
 
 __device__ __forceinline__ void tile_zero(Tile& t) {
@@ -240,7 +246,8 @@ __device__ __forceinline__ void tile_load_blk(Tile& t, const float* __restrict__
   for (int M = 0; M < 4; ++M)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float4 v = buf_load4(rs, vo, (M * 4 + q) * 1024);
+      u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (M * 4 + q) * 1024, PST_E_LOAD_AUX);
+      float4 v = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
       t.m[M][4 * q + 0] = v.x;
       t.m[M][4 * q + 1] = v.y;
       t.m[M][4 * q + 2] = v.z;

@@ -253,11 +253,24 @@ __device__ __forceinline__ int perm_pos(int c) {
   return h * 64 + M * 16 + r;
 }
 
+// acc = a_row + b_row (perm rows); b is streamed 4 values at a time so the sum needs one tile
+// of registers, not two
 __device__ __forceinline__ void tile_add_rows(Tile& acc, const float* __restrict__ a_row, const float* __restrict__ b_row) {
-  Tile t;
   tile_load_perm(acc, a_row);
-  tile_load_perm(t, b_row);
-  tile_add(acc, t);
+  const float4* p = reinterpret_cast<const float4*>(b_row + (lane_id() >> 5) * 64);
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#ifdef PST_STREAM_ADD
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      float4 v = p[M * 4 + q];
+      acc.m[M][4 * q + 0] = acc.m[M][4 * q + 0] + v.x;
+      acc.m[M][4 * q + 1] = acc.m[M][4 * q + 1] + v.y;
+      acc.m[M][4 * q + 2] = acc.m[M][4 * q + 2] + v.z;
+      acc.m[M][4 * q + 3] = acc.m[M][4 * q + 3] + v.w;
+    }
 }
 
 // 3-layer edge MLP starting from acc = init (Ps[s] + Pr[r], Pr's chain started from b0):
@@ -275,7 +288,15 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   __shared__ float lds_scratch[4][32 * 36];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (no waterfalls)
+#ifdef PST_XCD_REMAP
+  // blocks sharing an XCD (same blockIdx % 8) take a contiguous range of tasks, so the two
+  // workgroups of a protein (and its sender rows) share one L2 (bijective for any grid size)
+  const int nwg = gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = blockIdx.x % 8;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (int)(blockIdx.x / 8);
+  const int64_t task = (int64_t)wg * 4 + w;
+#else
   const int64_t task = (int64_t)blockIdx.x * 4 + w;
+#endif
   if (task >= a.n_tasks) return;
   const int64_t g0 = task * 32;
   float* scratch = lds_scratch[w];
