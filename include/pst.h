@@ -151,6 +151,29 @@ int pst_codebook_aux_device(pst_ctx* ctx, float* d_distances, float* d_soft_prob
 
 int pst_sync(pst_ctx* ctx);
 
+/*
+ * Native PDB parsing (host, no GPU): replaces protein_structure_from_pdb_string
+ * (structure_tokenizer/data/protein_structure_sample.py:166-248, Biopython PDBParser semantics,
+ * restated in pst_amd/pdb.py) for make_graph_from_pdb (scripts/inference_runner.py:47-50).
+ * n inputs are parsed on n_threads host threads into a batch handle; chain_id = 0 parses all
+ * chains, else only that chain. A failing input (multi-model, insertion code, malformed
+ * record, unreadable file) gets status PST_E_INVALID and 0 residues; the others are unaffected.
+ */
+typedef struct pst_pdb_batch pst_pdb_batch;
+int pst_pdb_parse_files(const char* const* paths, int32_t n, char chain_id, int32_t n_threads,
+                        pst_pdb_batch** out);
+int pst_pdb_parse_strings(const char* const* texts, const size_t* lens, int32_t n, char chain_id,
+                          int32_t n_threads, pst_pdb_batch** out);
+/* number of inputs and total residues kept */
+int pst_pdb_batch_sizes(const pst_pdb_batch* b, int32_t* n, int64_t* n_residues);
+/* Copy out the packed batch (any pointer may be NULL):
+ *   positions [R,37,3] f64, flags [R,37] u8 (bit0 gt_exists, bit1 atom_exists),
+ *   aatype [R] u8 (restype index, 20 = UNK), offsets [n+1] i64, status [n] i32 */
+int pst_pdb_batch_copy(const pst_pdb_batch* b, double* positions, uint8_t* flags, uint8_t* aatype,
+                       int64_t* offsets, int32_t* status);
+const char* pst_pdb_batch_error(const pst_pdb_batch* b, int32_t i);
+void pst_pdb_batch_free(pst_pdb_batch* b);
+
 /* Per-stage timing of the last tokenize call (HIP events on the context's stream):
  * ms[0..5] = prep, knn, mpnn layer 0, mpnn layer 1, mpnn layer 2, downsampler+FSQ. */
 #define PST_N_STAGES 6

@@ -7,7 +7,7 @@ HIP device is missing, loading raises.
 import ctypes
 import os
 import sys
-from typing import List, Optional, Sequence, Tuple
+from typing import List, NamedTuple, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -36,7 +36,8 @@ _lib = None
 EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "pst_create_error",
            "pst_tokenize", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
            "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing", "pst_device_count",
-           "pst_codebook_aux_device")
+           "pst_codebook_aux_device", "pst_pdb_parse_files", "pst_pdb_parse_strings",
+           "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -82,6 +83,13 @@ def lib():
         L.pst_set_timing.argtypes = [P, ctypes.c_int32]
         L.pst_get_timing.argtypes = [P, P]
         L.pst_device_count.argtypes = [P]
+        L.pst_pdb_parse_files.argtypes = [P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
+        L.pst_pdb_parse_strings.argtypes = [P, P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
+        L.pst_pdb_batch_sizes.argtypes = [P, P, P]
+        L.pst_pdb_batch_copy.argtypes = [P, P, P, P, P, P]
+        L.pst_pdb_batch_error.restype = ctypes.c_char_p
+        L.pst_pdb_batch_error.argtypes = [P, ctypes.c_int32]
+        L.pst_pdb_batch_free.argtypes = [P]
         _lib = L
     return _lib
 
@@ -106,6 +114,70 @@ def raise_for(code: int, msg: str):
     if code == PST_E_INVALID:
         raise ValueError(msg)
     raise PstError(f"libpst error {code}: {msg}")
+
+
+class PdbBatch(NamedTuple):
+    """Packed result of the native parser (pst_pdb_parse_*): ragged atom37 arrays in input order."""
+    positions: np.ndarray  # [R,37,3] f64
+    flags: np.ndarray      # [R,37] u8
+    aatype: np.ndarray     # [R] u8
+    offsets: np.ndarray    # [n+1] i64
+    status: np.ndarray     # [n] i32 (0 ok)
+    errors: List[str]
+
+    def sample(self, i: int):
+        """Input i as a ProteinStructureSample (raises ValueError with the parser's message)."""
+        from .sample import ProteinStructureSample
+        if self.status[i] != PST_OK:
+            raise ValueError(self.errors[i])
+        a, b = int(self.offsets[i]), int(self.offsets[i + 1])
+        n = b - a
+        onehot = np.zeros((n, 21))
+        onehot[np.arange(n), self.aatype[a:b]] = 1.0
+        fl = self.flags[a:b]
+        return ProteinStructureSample(None, n, onehot, self.positions[a:b], (fl & 1).astype(bool),
+                                      ((fl >> 1) & 1).astype(bool), 0.0, 1)
+
+
+def _collect_pdb(h) -> PdbBatch:
+    L = lib()
+    try:
+        n = ctypes.c_int32()
+        r = ctypes.c_int64()
+        L.pst_pdb_batch_sizes(h, ctypes.byref(n), ctypes.byref(r))
+        n, r = n.value, r.value
+        pos = np.zeros((r, 37, 3), np.float64)
+        fl = np.zeros((r, 37), np.uint8)
+        aa = np.zeros(r, np.uint8)
+        off = np.zeros(n + 1, np.int64)
+        st = np.zeros(n, np.int32)
+        L.pst_pdb_batch_copy(h, _ptr(pos), _ptr(fl), _ptr(aa), _ptr(off), _ptr(st))
+        errs = [L.pst_pdb_batch_error(h, i).decode() for i in range(n)]
+    finally:
+        L.pst_pdb_batch_free(h)
+    return PdbBatch(pos, fl, aa, off, st, errs)
+
+
+def parse_pdb_files(paths: Sequence[str], chain_id: Optional[str] = None, n_threads: int = 8) -> PdbBatch:
+    """Parse PDB files on n_threads host threads with the native parser (pst_pdb_parse_files)."""
+    enc = [os.fsencode(p) for p in paths]
+    arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+    h = ctypes.c_void_p()
+    rc = lib().pst_pdb_parse_files(arr, len(enc), (chain_id or "\0").encode()[:1], n_threads, ctypes.byref(h))
+    if rc != PST_OK:
+        raise PstError(f"pst_pdb_parse_files failed: {rc}")
+    return _collect_pdb(h)
+
+
+def parse_pdb_strings(texts: Sequence[str], chain_id: Optional[str] = None, n_threads: int = 8) -> PdbBatch:
+    enc = [t.encode() for t in texts]
+    arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+    lens = (ctypes.c_size_t * max(len(enc), 1))(*[len(e) for e in enc])
+    h = ctypes.c_void_p()
+    rc = lib().pst_pdb_parse_strings(arr, lens, len(enc), (chain_id or "\0").encode()[:1], n_threads, ctypes.byref(h))
+    if rc != PST_OK:
+        raise PstError(f"pst_pdb_parse_strings failed: {rc}")
+    return _collect_pdb(h)
 
 
 def pack_samples(samples) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

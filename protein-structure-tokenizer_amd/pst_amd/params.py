@@ -2,8 +2,8 @@
 
 Names are the haiku paths the reference creates for `Vq3D.encode_and_quantize` after
 `params_keys_conversion` strips `forward_vq3_d/` (`scripts/inference_runner.py:153-165`);
-`tests/test_golden_host.py` checks them against the reference model initialised under the
-test shim. The blob is every tensor below, row-major, concatenated in `param_spec` order — the
+`tests/test_params.py` checks them (and the decoder half) against the reference model
+initialised under the test shim (`tests/golden/full_param_names.json`). The blob is every tensor below, row-major, concatenated in `param_spec` order — the
 layout `include/pst.h` documents (`pst_param_count`).
 """
 import os

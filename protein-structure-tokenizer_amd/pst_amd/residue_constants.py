@@ -3,7 +3,7 @@
 Mirrors the subset of `structure_tokenizer/data/residue_constants.py` that the PDB parser and
 graph builder read: the atom37 ordering (`:539-579`), the 20-letter restype order (`:706-729`),
 the 1<->3 letter maps (`:812-840`) and `res_atom37_exist` (`:733-737`, UNK = N, CA, C, CB).
-`tests/test_golden_host.py` checks every table against the reference module.
+`tests/test_reference_tables.py` checks every table against the reference module.
 """
 from typing import Dict, List
 

@@ -30,23 +30,29 @@ import numpy as np
 from . import _native
 from . import params as _params
 from .config import LEVELS, TokenizerConfig
-from .pdb import protein_structure_from_pdb_string
 from .sample import ProteinStructureSample
+
+
+PARSE_THREADS = int(os.environ.get("PST_PARSE_THREADS", "8"))
 
 
 # ------------------------------------------------------------------------------- graph inputs
 def make_graph_from_pdb(pdb_file_path: str, num_neighbor: int, downsampling_ratio: int,
-                        residue_loc_is_alphac: bool, padding_num_residue: int) -> ProteinStructureSample:
+                        residue_loc_is_alphac: bool, padding_num_residue: int,
+                        sample: Optional[ProteinStructureSample] = None) -> ProteinStructureSample:
     """Parse one PDB and apply the reference's size gates (`inference_runner.py:40-74`).
 
     Returns the parsed structure; the residue graph (`preprocess_sample`) is built on the GPU
-    by `pst_tokenize`, so nothing else happens on the host. `residue_loc_is_alphac=False` and
-    other `padding_num_residue` / `num_neighbor` values than the shipped 512 / 50 are rejected
-    (the device kernels are specialised for them).
+    by `pst_tokenize`, so nothing else happens on the host. Parsing uses libpst's native
+    parser (`pst_pdb_parse_files`, Biopython semantics as restated in `pst_amd/pdb.py`);
+    `sample` skips parsing when the caller parsed a batch already. `residue_loc_is_alphac=False`
+    and other `padding_num_residue` / `num_neighbor` values than the shipped 512 / 50 are
+    rejected (the device kernels are specialised for them).
     """
-    with open(pdb_file_path, "r") as file:
-        pdb_content = file.read()
-    sample = protein_structure_from_pdb_string(pdb_content)
+    if sample is None:
+        if not os.path.exists(pdb_file_path):
+            raise FileNotFoundError(pdb_file_path)
+        sample = _native.parse_pdb_files([pdb_file_path], n_threads=1).sample(0)
     if sample.nb_residues > 512:
         raise NotImplementedError(
             "We currently don't support protein with more than 512 residues"
@@ -284,10 +290,15 @@ class InferenceRunner:
 
         def load(it):
             files = pdbs[it * effective_batch_size:(it + 1) * effective_batch_size]
+            for f in files:
+                if not os.path.exists(f):
+                    raise FileNotFoundError(f)
+            parsed = _native.parse_pdb_files(files, n_threads=PARSE_THREADS)
             graphs = [make_graph_from_pdb(pdb_file_path=f, num_neighbor=data_config.graph_max_neighbor,
                                           downsampling_ratio=data_config.downsampling_ratio,
                                           residue_loc_is_alphac=data_config.residue_loc_is_alphac,
-                                          padding_num_residue=data_config.seq_max_size) for f in files]
+                                          padding_num_residue=data_config.seq_max_size,
+                                          sample=parsed.sample(i)) for i, f in enumerate(files)]
             return files, batch_collate([num_device, batch_size_per_device], graphs)
 
         with _cf.ThreadPoolExecutor(max_workers=1) as io:

@@ -208,3 +208,82 @@ def test_shard_for_rank_partitions():
     assert all(len(set(a) & set(b)) == 0 for i, a in enumerate(parts) for b in parts[i + 1:])
     with pytest.raises(ValueError):
         runner.shard_for_rank(items, 3, 3)
+
+
+# ------------------------------------------------------------------------------ native parser
+def _both(txt, chain_id=None):
+    from pst_amd import _native
+    nat = _native.parse_pdb_strings([txt], chain_id=chain_id, n_threads=1)
+    try:
+        py = pdb.protein_structure_from_pdb_string(txt, chain_id=chain_id)
+    except ValueError as e:
+        assert nat.status[0] != 0
+        assert nat.errors[0] == str(e)
+        return None
+    s = nat.sample(0)
+    assert s.nb_residues == py.nb_residues
+    assert np.array_equal(s.atom37_positions, py.atom37_positions)
+    assert np.array_equal(s.atom37_gt_exists, py.atom37_gt_exists)
+    assert np.array_equal(s.atom37_atom_exists, py.atom37_atom_exists)
+    assert np.array_equal(s.aatype, py.aatype)
+    return s
+
+
+def _edge_texts():
+    alt = _res("A", 1, "ALA") + [_atom(9, "CB", "ALA", "A", 1, 5.0, 5.0, 5.0, occ=0.3, altloc="A"),
+                                 _atom(10, "CB", "ALA", "A", 1, 6.0, 6.0, 6.0, occ=0.7, altloc="B"),
+                                 _atom(11, "CB", "ALA", "A", 1, 7.0, 7.0, 7.0, occ=0.7, altloc="C")]
+    het = (_res("A", 1) + _res("A", 2, "MSE", base=10.0, rec="HETATM")
+           + [_atom(20, "O", "HOH", "A", 3, 1.0, 1.0, 1.0, rec="HETATM"),
+              _atom(21, "ZN", "ZN", "A", 4, 1.0, 1.0, 1.0, rec="HETATM")])
+    return {
+        "altloc": "\n".join(alt),
+        "hetero": "\n".join(het),
+        "chains": "\n".join(_res("B", 1) + _res("A", 1, base=5.0) + _res("B", 2, base=9.0)),
+        "multimodel": "\n".join(["MODEL        1"] + _res("A", 1) + ["ENDMDL", "MODEL        2"] + _res("A", 1) + ["ENDMDL"]),
+        "onemodel": "\n".join(["MODEL        1"] + _res("A", 1) + ["ENDMDL"]),
+        "icode": "\n".join(_res("A", 1) + _res("A", 1, icode="B")),
+        "crlf": "\r\n".join(_res("A", 1) + _res("A", 2, base=3.0)),
+        "empty": "HEADER    nothing\nEND\n",
+        "same_key_het_vs_atom": "\n".join(_res("A", 5) + _res("A", 5, "GLY", base=2.0, rec="HETATM")),
+    }
+
+
+@pytest.mark.parametrize("case", sorted(_edge_texts()))
+def test_native_parser_matches_restatement(case):
+    _both(_edge_texts()[case])
+
+
+def test_native_parser_chain_filter_and_synthetic():
+    assert _both(_edge_texts()["chains"], chain_id="A").nb_residues == 1
+    for i, n in enumerate((50, 77, 130)):
+        s = synthetic.synthetic_protein(n, 60 + i)
+        got = _both(pdb.to_pdb_string(s))
+        assert np.array_equal(got.atom37_positions, s.atom37_positions)
+
+
+def test_native_parser_batch_errors_are_per_input(tmp_path):
+    from pst_amd import _native
+    good = tmp_path / "good.pdb"
+    good.write_text(pdb.to_pdb_string(synthetic.synthetic_protein(55, 3)))
+    bad = tmp_path / "bad.pdb"
+    bad.write_text(_edge_texts()["multimodel"])
+    B = _native.parse_pdb_files([str(good), str(bad), str(tmp_path / "missing.pdb"), str(good)], n_threads=3)
+    assert B.status.tolist() == [0, -1, -1, 0]
+    assert np.diff(B.offsets).tolist() == [55, 0, 0, 55]
+    assert "single model" in B.errors[1] and "missing.pdb" in B.errors[2]
+    with pytest.raises(ValueError, match="single model"):
+        B.sample(1)
+
+
+@pytest.mark.reference
+def test_native_parser_casp14_equals_restatement():
+    import glob
+    import _refenv
+    from pst_amd import _native
+    files = sorted(glob.glob(os.path.join(_refenv.REF, "casp14_pdbs", "*.pdb")))
+    B = _native.parse_pdb_files(files, n_threads=4)
+    F = np.load(os.path.join(GOLD, "casp14_atom37.npz"))
+    assert np.array_equal(B.offsets, F["offsets"])
+    assert np.array_equal(B.positions, F["positions"].astype(np.float64))
+    assert np.array_equal(B.flags, F["flags"])
