@@ -58,6 +58,35 @@ def parse():
     return ap.parse_args()
 
 
+def casp14_end_to_end(tk):
+    """SURVEY config 2 as the CLI runs it: parse the 31 CASP14 PDB files (native parser, 16
+    threads), tokenize from host buffers, write <stem>_tokens.npy. Reported beside `value`."""
+    import tarfile
+    import tempfile
+    from pst_amd._native import parse_pdb_files
+    arc = os.path.join(ROOT, "tests", "golden", "casp14_pdbs.tar.gz")
+    if not os.path.exists(arc):
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        with tarfile.open(arc) as tf:
+            tf.extractall(d, members=[m for m in tf.getmembers() if m.isfile() and m.name.endswith(".pdb")])
+        files = sorted(os.path.join(d, "casp14_pdbs", f) for f in os.listdir(os.path.join(d, "casp14_pdbs")))
+        os.makedirs(os.path.join(d, "out"))
+        t0 = time.perf_counter()
+        B = parse_pdb_files(files, n_threads=16)
+        t1 = time.perf_counter()
+        tok, nt, _ = tk.tokenize_packed(B.positions, B.flags, B.offsets)
+        t2 = time.perf_counter()
+        for i, f in enumerate(files):
+            a = int(B.offsets[i])
+            np.save(os.path.join(d, "out", os.path.basename(f)[:-4] + "_tokens"), tok[a:a + nt[i]].reshape(1, -1))
+        t3 = time.perf_counter()
+    R = int(B.offsets[-1])
+    return {"workload": "CASP14 31 structures (SURVEY config 2), codebook 4096, df 1", "residues": R,
+            "parse_ms": round((t1 - t0) * 1e3, 2), "tokenize_ms": round((t2 - t1) * 1e3, 2),
+            "write_ms": round((t3 - t2) * 1e3, 2), "residues_per_s": round(R / (t3 - t0), 1)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,6 +177,8 @@ def main():
     tk.tokenize_packed(pos, flags, off)
     pcie_rate = residues_per_rank / (time.perf_counter() - t2)
 
+    e2e = casp14_end_to_end(tk) if (rank == 0 and world == 1) else None
+
     cpu = None
     exact = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -186,6 +217,7 @@ def main():
             "cpu_baseline": cpu,
             "exact_match": exact,
             "pcie_inclusive_residues_per_s_per_gpu": round(pcie_rate, 1),
+            "casp14_end_to_end": e2e,
         }
         print(json.dumps(out), flush=True)
     tk.close()

@@ -26,3 +26,15 @@ def pytest_collection_modifyitems(config, items):
 
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+@pytest.fixture(scope="session")
+def casp14_dir(tmp_path_factory):
+    """The 31 CASP14 PDB files (tests/golden/casp14_pdbs.tar.gz) extracted to a temp dir."""
+    import tarfile
+    d = tmp_path_factory.mktemp("casp14")
+    with tarfile.open(os.path.join(GOLDEN, "casp14_pdbs.tar.gz")) as tf:
+        for m in tf.getmembers():
+            if m.isfile() and m.name.startswith("casp14_pdbs/") and m.name.endswith(".pdb") and ".." not in m.name:
+                tf.extract(m, d)
+    return os.path.join(str(d), "casp14_pdbs")

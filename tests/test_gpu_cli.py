@@ -83,3 +83,34 @@ def test_tokenize_fn_emit_aux_matches_reference_golden():
     assert abs(out["perplexity"][0] - float(F[c + "perplexity"])) < 1e-4 * float(F[c + "perplexity"])
     assert np.all(out["distances"][0, 0, T:] == 0) and np.all(out["quantize"][0, 0, T:] == 0)
     np.testing.assert_allclose(out["soft_proba"][0, 0, T:].sum(-1), 1.0, rtol=1e-5)
+
+
+@pytest.mark.parametrize("subset", ["T1024", "all"])
+def test_cli_casp14(tmp_path, casp14_dir, subset):
+    """SURVEY configs 1 (T1024, 391 tokens) and 2 (all 31 structures) through the drop-in CLI."""
+    import shutil
+    sys.path.insert(0, SCRIPTS)
+    import tokenize_pdb
+    pdb_dir = tmp_path / "pdbs"
+    pdb_dir.mkdir()
+    names = ["T1024"] if subset == "T1024" else sorted(f[:-4] for f in os.listdir(casp14_dir))
+    for nm in names:
+        shutil.copy(os.path.join(casp14_dir, nm + ".pdb"), pdb_dir / (nm + ".pdb"))
+    mdir = tmp_path / "model"
+    mdir.mkdir()
+    full = P.random_full_params(6, seed=8)
+    P.save_params_npz(str(mdir / "params.npz"), full)
+    out = tmp_path / "tokens"
+    tokenize_pdb.cli(["--pdb_dir", str(pdb_dir), "--token_save_path", str(out), "--batch_size_per_device", "8",
+                      "--weights_dir", str(mdir)])
+    blob = P.pack(full, 6)
+    F = np.load(os.path.join(os.path.dirname(__file__), "golden", "casp14_atom37.npz"))
+    idx = {str(n): i for i, n in enumerate(F["names"])}
+    for nm in names:
+        i = idx[nm]
+        a, b = int(F["offsets"][i]), int(F["offsets"][i + 1])
+        want = O.tokenize(blob, C.LEVELS[4096], 1, F["positions"][a:b].astype(np.float64), F["flags"][a:b])["tokens"]
+        t = np.load(out / f"{nm}_tokens.npy")
+        assert np.array_equal(t[0], want), nm
+    if subset == "T1024":
+        assert np.load(out / "T1024_tokens.npy").shape == (1, 391)

@@ -287,3 +287,15 @@ def test_native_parser_casp14_equals_restatement():
     assert np.array_equal(B.offsets, F["offsets"])
     assert np.array_equal(B.positions, F["positions"].astype(np.float64))
     assert np.array_equal(B.flags, F["flags"])
+
+
+def test_native_parser_casp14_archive(casp14_dir):
+    from pst_amd import _native
+    files = sorted(os.path.join(casp14_dir, f) for f in os.listdir(casp14_dir))
+    assert len(files) == 31
+    B = _native.parse_pdb_files(files, n_threads=4)
+    F = np.load(os.path.join(GOLD, "casp14_atom37.npz"))
+    assert [os.path.basename(f)[:-4] for f in files] == [str(x) for x in F["names"]]
+    assert np.array_equal(B.offsets, F["offsets"])
+    assert np.array_equal(B.positions, F["positions"].astype(np.float64))
+    assert np.array_equal(B.flags, F["flags"])
