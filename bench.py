@@ -38,7 +38,7 @@ H, K = 128, 50
 # k_mpnn<1> = edge MLP of layer 1 + message MLP of layer 2 over 50 edges, + layer-2 node FFN:
 MLP_FLOP = 2 * (3 * H * H + H * H + H * H)          # 163 840 per edge per 384-128-128-128 MLP
 MPNN1_ALG_FLOP_PER_RES = K * 2 * MLP_FLOP + 2 * (H * 4 * H + 4 * H * H)   # 16 646 144
-PATH_ALG_FLOP_PER_RES = 44_715_008                  # SURVEY §8d, whole path at df = 1
+PATH_ALG_FLOP_PER_RES = {1: 44_715_008, 4: 44_395_904}  # SURVEY §8d, whole path per residue
 # What k_mpnn<1> executes (node-projection split of the 384-wide first layers)
 MPNN1_EXEC_FLOP_PER_RES = K * 6 * 2 * H * H + 4 * 2 * H * H + 2 * (H * 4 * H + 4 * H * H)
 
@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--proteins", type=int, default=N_PROT)
     ap.add_argument("--residues", type=int, default=N_RES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the CASP14 end-to-end field")
+    ap.add_argument("--codebook", type=int, default=CODEBOOK, help="secondary configs (default: the metric's 4096)")
+    ap.add_argument("--df", type=int, default=DF)
     ap.add_argument("--cpu-sample", type=int, default=256, help="proteins in the CPU-baseline sample")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_k_mpnn1.json"),
                     help="PMC-measured HBM bytes per residue of k_mpnn<1> (tools/pmc_traffic.sh)")
@@ -106,8 +109,10 @@ def main():
     d_tok = torch.zeros(R, dtype=torch.int32, device=dev)
     d_ntok = torch.zeros(len(samples), dtype=torch.int32, device=dev)
     d_nn = torch.zeros(len(samples), dtype=torch.int32, device=dev)
-    blob = P.random_blob(6, 1234)
-    tk = Tokenizer(local, CODEBOOK, DF, blob)
+    from pst_amd.config import LEVELS
+    levels = LEVELS[args.codebook]
+    blob = P.random_blob(len(levels), 1234)
+    tk = Tokenizer(local, args.codebook, args.df, blob)
     torch.cuda.synchronize(dev)
 
     def step():
@@ -169,7 +174,8 @@ def main():
         "executed_tflops": round(executed, 2),
         "frac_executed": round(executed / PEAK_FP32_TFLOPS, 4),
         "stage_ms": {k: round(v, 3) for k, v in stage.items()},
-        "path_alg_tflops": round(PATH_ALG_FLOP_PER_RES * residues_per_rank / (sum(stage.values()) * 1e-3) / 1e12, 2),
+        "path_alg_tflops": (round(PATH_ALG_FLOP_PER_RES[args.df] * residues_per_rank / (sum(stage.values()) * 1e-3) / 1e12, 2)
+                            if args.df in PATH_ALG_FLOP_PER_RES else None),
     }
 
     # PCIe-inclusive rate: host buffers in, host token ids out (pst_tokenize); never `value`
@@ -177,7 +183,7 @@ def main():
     tk.tokenize_packed(pos, flags, off)
     pcie_rate = residues_per_rank / (time.perf_counter() - t2)
 
-    e2e = casp14_end_to_end(tk) if (rank == 0 and world == 1) else None
+    e2e = casp14_end_to_end(tk) if (rank == 0 and world == 1 and not args.no_e2e) else None
 
     cpu = None
     exact = None
@@ -187,7 +193,7 @@ def main():
         sub_off = off[:n + 1]
         sub_R = int(sub_off[-1])
         t1 = time.perf_counter()
-        otok, ont = O.tokenize_batch(blob, (4,) * 6, DF, pos[:sub_R], flags[:sub_R], sub_off, n_threads=args.cpu_threads)
+        otok, ont = O.tokenize_batch(blob, levels, args.df, pos[:sub_R], flags[:sub_R], sub_off, n_threads=args.cpu_threads)
         cpu_s = time.perf_counter() - t1
         cpu = {"value": round(sub_R / cpu_s, 1), "unit": "residues/s", "cores": args.cpu_threads, "kind": "port",
                "sample": f"first {n} of the synthetic proteins ({sub_R} residues), oracle/pst_oracle.c, "
@@ -198,7 +204,7 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "residues tokenized/sec (cb=4096, df=1)",
+            "metric": f"residues tokenized/sec (cb={args.codebook}, df={args.df})",
             "value": round(value, 1),
             "unit": "residues/s",
             "n_gpus": world,
@@ -210,8 +216,8 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (random-walk backbones, random-init weights of the reference architecture)",
-            "config": {"workload": f"{args.proteins} proteins x {args.residues} residues per GPU, codebook 4096, df 1",
-                       "codebook_size": CODEBOOK, "df": DF, "proteins_per_gpu": args.proteins,
+            "config": {"workload": f"{args.proteins} proteins x {args.residues} residues per GPU, codebook {args.codebook}, df {args.df}",
+                       "codebook_size": args.codebook, "df": args.df, "proteins_per_gpu": args.proteins,
                        "residues_per_protein": args.residues, "parallelism": f"dp{world} (independent proteins)"},
             "roofline": roofline,
             "cpu_baseline": cpu,
