@@ -61,6 +61,9 @@ def make_graph_from_pdb(pdb_file_path: str, num_neighbor: int, downsampling_rati
         raise NotImplementedError(
             f"We currently don't support protein with less than {num_neighbor} residues"
             f"given: {sample.nb_residues}")
+    if bool(np.all(sample.get_missing_backbone_coords_mask())):
+        # the reference fails in preprocess_sample (np.stack of no residues) with this message
+        raise ValueError("need at least one array to stack")
     if not residue_loc_is_alphac:
         raise NotImplementedError("libpst builds the graph on C-alpha locations only "
                                   "(graph_residue_loc_is_alphac: true in every shipped config)")

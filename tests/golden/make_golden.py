@@ -92,6 +92,12 @@ def main():
     pos_ = s.atom37_positions.copy()
     pos_[~gt] = 0.0
     syn["syn56_missing9"] = s._replace(atom37_gt_exists=gt, atom37_positions=pos_)
+    # tiny graphs: only the first 5 / 1 residues keep their O atom (n = 5, n = 1)
+    for keep in (5, 1):
+        s = synthetic.synthetic_protein(60, 12 + keep)
+        gt = s.atom37_gt_exists.copy()
+        gt[keep:, rc.O_INDEX] = False
+        syn[f"syn60_keep{keep}"] = s._replace(atom37_gt_exists=gt)
     for k, v in syn.items():
         cases[k + "_df1"] = (v, 1)
     cases["syn130_df4"] = (syn["syn130"], 4)
@@ -109,7 +115,7 @@ def main():
     # --- FSQ index map: reference codes_to_indexes / indexes_to_codes -------------------
     from structure_tokenizer.model import quantize as ref_q
     fsq = {}
-    for levels in ([4] * 6, [8, 8, 8, 5, 5, 5], [8, 6, 5], [8, 8, 6, 5]):
+    for levels in ([4] * 6, [8, 8, 8, 5, 5, 5], [4, 4, 3, 3, 3], [4, 4, 4, 3, 3, 3]):
         lv = np.asarray(levels)
         k = int(np.prod(lv))
         basis = np.concatenate(([1], np.cumprod(lv[:-1]))).astype(np.uint32)

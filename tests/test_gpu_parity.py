@@ -123,3 +123,67 @@ def test_size_gates_raise_like_reference():
         tk.tokenize([synthetic.synthetic_protein(513, 1)])
     with pytest.raises(NotImplementedError):
         tk.tokenize([synthetic.synthetic_protein(49, 1)])
+
+
+def test_graph_bitwise_vs_reference_fixtures():
+    """Every graph_golden case (reference preprocess_sample run under the shim) in one ragged batch,
+    plus a protein whose residues all lack backbone (n = 0): senders and edge features bitwise."""
+    G = np.load(os.path.join(GOLD, "graph_golden.npz"))
+    cases = sorted(k.split("/")[0] for k in G.files if k.endswith("/n_node"))
+    cases = [c for c in cases if int(G[c + "/df"]) == 1]
+    samples = [_samples_from(G, c) for c in cases]
+    empty = synthetic.synthetic_protein(60, 5)
+    gt = empty.atom37_gt_exists.copy()
+    gt[:, 4] = False
+    ie = len(samples) // 2
+    samples.insert(ie, empty._replace(atom37_gt_exists=gt))
+    tk = tokenizer(4096, 1)
+    from pst_amd._native import pack_samples
+    pos, flags, off = pack_samples(samples)
+    tok, nt, nn = tk.tokenize_packed(pos, flags, off)
+    R = int(off[-1])
+    feat = tk.debug_fetch(10, R)
+    snd = tk.debug_fetch(11, R)
+    gi = 0
+    for b, s in enumerate(samples):
+        if b == ie:
+            assert nn[b] == 0 and nt[b] == 0
+            continue
+        c = cases[gi]
+        gi += 1
+        n = int(G[c + "/n_node"])
+        assert nn[b] == n, c
+        k = 50
+        slots = np.arange(n * k)
+        r, j = slots // k, slots % k
+        deg = min(n, k)
+        valid = j < deg
+        base = int(off[b])
+        got_s = snd[base * k: (base + n) * k] - base
+        assert np.array_equal(got_s[valid], G[c + "/senders"][valid]), c
+        got_f = feat[base * k: (base + n) * k, :27]
+        assert np.array_equal(np.ascontiguousarray(got_f).view(np.uint32), G[c + "/edge_features"].view(np.uint32)), c
+    assert gi == len(cases)
+
+
+@pytest.mark.parametrize("df", [1, 4])
+def test_tiny_and_empty_proteins(df):
+    """n = 0, 1, 3, 5 usable residues (R = 60 raw each) next to a normal protein."""
+    samples = []
+    for keep in (0, 1, 3, 5):
+        s = synthetic.synthetic_protein(60, 40 + keep)
+        gt = s.atom37_gt_exists.copy()
+        gt[keep:, 4] = False
+        samples.append(s._replace(atom37_gt_exists=gt))
+    samples.append(synthetic.synthetic_protein(90, 3))
+    cb = 64000 if df == 4 else 4096
+    tk = tokenizer(cb, df)
+    from pst_amd._native import pack_samples
+    pos, flags, off = pack_samples(samples)
+    tok, nt, nn = tk.tokenize_packed(pos, flags, off)
+    assert nn.tolist() == [0, 1, 3, 5, 90]
+    assert nt.tolist() == [n // df for n in (0, 1, 3, 5, 90)]
+    blob = P.random_blob(len(LEVELS[cb]), 1234)
+    for b, s in enumerate(samples):
+        o = O.tokenize(blob, LEVELS[cb], df, s.atom37_positions, s.atom_flags())
+        assert np.array_equal(tok[off[b]: off[b] + nt[b]], o["tokens"])

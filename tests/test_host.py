@@ -299,3 +299,13 @@ def test_native_parser_casp14_archive(casp14_dir):
     assert np.array_equal(B.offsets, F["offsets"])
     assert np.array_equal(B.positions, F["positions"].astype(np.float64))
     assert np.array_equal(B.flags, F["flags"])
+
+
+def test_make_graph_no_backbone_raises_like_reference(tmp_path):
+    s = synthetic.synthetic_protein(60, 2)
+    gt = s.atom37_gt_exists.copy()
+    gt[:, 4] = False  # every residue lacks O → reference preprocess_sample fails
+    p = _write(tmp_path, "noo.pdb", s._replace(atom37_gt_exists=gt))
+    with pytest.raises(ValueError, match="need at least one array"):
+        runner.make_graph_from_pdb(p, num_neighbor=50, downsampling_ratio=1, residue_loc_is_alphac=True,
+                                   padding_num_residue=512)
