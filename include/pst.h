@@ -152,6 +152,32 @@ int pst_codebook_aux_device(pst_ctx* ctx, float* d_distances, float* d_soft_prob
 int pst_sync(pst_ctx* ctx);
 
 /*
+ * Decode path (token ids → backbone structure): replaces InferenceRunner.prepare_decode_fn /
+ * prepare_token_to_code_fn / decode_and_save_pdbs (scripts/inference_runner.py:193-233, 326-437),
+ * i.e. Vq3D.indexes_to_codes + decode + structure_module (model/model.py:261-262, 481-569).
+ * The decoder-half parameter blob is every tensor of pst_amd.params.decoder_param_spec, row-major,
+ * concatenated in that order (up_proj, cross_attn_upsampling, sequence_decoder, structure_module).
+ */
+typedef struct pst_decoder pst_decoder;
+size_t pst_decoder_param_count(int32_t n_levels);
+int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* params, size_t n_params,
+                       pst_decoder** out);
+int pst_decoder_destroy(pst_decoder* dec);
+const char* pst_decoder_last_error(const pst_decoder* dec);
+const char* pst_decoder_create_error(void);
+/* Decode B proteins (host buffers, synchronous). Protein b's token ids are
+ * tokens[token_offsets[b] .. token_offsets[b+1]) (at most 512/df, ids < codebook size); it gets
+ * N_b = df · T_b residues. atom37_out [sum N_b, 37, 3] f32 receives final_atom_positions (N, CA,
+ * C and O set, every other atom 0 — the reference's dummy-ALA mask, model.py:547-568);
+ * n_nodes_out [B] (may be NULL) receives N_b. */
+int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* token_offsets,
+                       int32_t n_prot, float* atom37_out, int32_t* n_nodes_out);
+/* Intermediates of the last decode call (needs PST_DEBUG=1): which = 0 single [sum N,128],
+ * 1 pair [sum N², 128], 2 affine trajectory [per protein 8, N, 7], 3 torsion sin/cos
+ * [per protein 8, N, 3, 2], 4 atom14 [sum N, 14, 3]. */
+int pst_decoder_debug(pst_decoder* dec, int32_t which, float* out, size_t n_floats);
+
+/*
  * Native PDB parsing (host, no GPU): replaces protein_structure_from_pdb_string
  * (structure_tokenizer/data/protein_structure_sample.py:166-248, Biopython PDBParser semantics,
  * restated in pst_amd/pdb.py) for make_graph_from_pdb (scripts/inference_runner.py:47-50).

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/pst.h"
+#include "pst_pe.h"
 #include "pst_kernels.h"
 
 namespace {
@@ -154,21 +155,6 @@ std::vector<float> cat(std::initializer_list<std::vector<float>> parts) {
 }
 
 // positional_encoding_layer.py:49-66 with a float32 argument
-float pe_value(int x, int n, int k1) {
-  int num = (k1 & 1) ? 2 * (k1 - 1) : 2 * k1;
-  float e = (float)num / 128.0f;
-  float pw = (float)std::pow((double)n, (double)e);
-  float arg = ((float)x * 3.14159274101257324f) / pw;
-  return (float)((k1 & 1) ? std::cos((double)arg) : std::sin((double)arg));
-}
-
-std::vector<float> pe_rows(int x0, int count, int n) {
-  std::vector<float> out((size_t)count * 128);
-  for (int i = 0; i < count; ++i)
-    for (int k = 1; k <= 128; ++k) out[(size_t)i * 128 + k - 1] = pe_value(x0 + i, n, k);
-  return out;
-}
-
 struct MlpOff {
   size_t w0, b0, w1, b1, w2, b2, bf0, bf1, bf2;
 };
@@ -343,9 +329,9 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   for (int d = 0; d < ctx->D; ++d) db[d] = P.down.b[d];
   ctx->down_b = A.add(db);
   // staging inputs for the table GEMMs
-  auto nodePE = perm_rows(pe_rows(0, 512, 512), 512);
-  auto edgePE = perm_rows(pe_rows(-511, 1023, 512), 1023);
-  auto rpe = perm_rows(pe_rows(0, ctx->max_out, ctx->max_out), ctx->max_out);
+  auto nodePE = perm_rows(pst::pe_rows(0, 512, 512), 512);
+  auto edgePE = perm_rows(pst::pe_rows(-511, 1023, 512), 1023);
+  auto rpe = perm_rows(pst::pe_rows(0, ctx->max_out, ctx->max_out), ctx->max_out);
   size_t o_npe = A.add(nodePE), o_epe = A.add(edgePE);
   size_t o_ne_w = A.add(frag(P.node_embed.w, H, 0, 128, 128, 0, 128)), o_ne_b = A.add(perm(P.node_embed.b));
   size_t o_ee_w = A.add(frag(P.edge_embed.w, H, 0, 128, 128, 0, 128));

@@ -1,0 +1,946 @@
+// pst_decode.hip — token ids → backbone atom37 coordinates on the GPU (the reference's decode path:
+// Vq3D.indexes_to_codes → decode → structure_module, model/model.py:481-569 + folding.py), C ABI in
+// include/pst.h (pst_decoder_*).
+//
+// Per protein (T tokens, N = df·T nodes; only real rows are computed — every masked row/key of the
+// reference contributes exact zeros to them):
+//   codes → up_proj → "original" = Linear([PE(t; 512/df) | up])               modules.py:453-480
+//   3 cross-attention blocks: nodes (PE(i; 512) queries) attend over tokens, gated; transitions
+//                                                                              modules.py:537-636
+//   spherical norm → s; pair: LN → left/right (256) → P = left[i]⊙right[j] → LN(MLP(P) + Lin(P))
+//   → [PE(j−i) | pair] → Linear → Transition = z                    sequence_decoder.py, modules.py:639-740
+//   structure module: 8 fold iterations (IPA with pair bias and point attention, transitions,
+//   quaternion backbone update, backbone torsions → frames → atom14 → atom37)        folding.py
+// Kernels are plain fp32 (VALU fma chains, LDS-tiled GEMM); this path is not the benchmarked one.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/pst.h"
+#include "pst_backbone_tables.h"
+#include "pst_pe.h"
+
+namespace pst {
+namespace dec {
+
+enum { F_RELU_OUT = 1, F_RELU_IN = 2, F_ACCUM = 4, F_SIGMOID_OUT = 8 };
+
+__global__ void k_scale(float* x, int64_t n, float s) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = x[i] * s;
+}
+__global__ void k_add(float* x, const float* y, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = x[i] + y[i];
+}
+__global__ void k_zero(float* x, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = 0.0f;
+}
+
+// Y[M,N] (op)= act(act_in(X[M,K]) · W[K,N] + b): fp32 fma chain over k ascending, 64×64 tile per
+// workgroup, 4×4 outputs per thread, K staged through LDS 16 at a time.
+__global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ X, int ldx, const float* __restrict__ W,
+                                              int ldw, const float* __restrict__ b, float* __restrict__ Y, int ldy,
+                                              int M, int N, int K, int flags) {
+  __shared__ float Xs[16][64 + 1];
+  __shared__ float Ws[16][64];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int row0 = blockIdx.y * 64, col0 = blockIdx.x * 64;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+      int r = e >> 4, kk = e & 15;
+      int gr = row0 + r, gk = k0 + kk;
+      float v = (gr < M && gk < K) ? X[(int64_t)gr * ldx + gk] : 0.0f;
+      if (flags & F_RELU_IN) v = v > 0.0f ? v : 0.0f;
+      Xs[kk][r] = v;
+      int wk = e >> 6, wc = e & 63;
+      int gwk = k0 + wk, gwc = col0 + wc;
+      Ws[wk][wc] = (gwk < K && gwc < N) ? W[(int64_t)gwk * ldw + gwc] : 0.0f;
+    }
+    __syncthreads();
+    const int kmax = min(16, K - k0);
+    for (int kk = 0; kk < kmax; ++kk) {
+      float xv[4], wv[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) xv[a] = Xs[kk][ty * 4 + a];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wv[c] = Ws[kk][tx * 4 + c];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[a][c] = __builtin_fmaf(xv[a], wv[c], acc[a][c]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int r = row0 + ty * 4 + a;
+    if (r >= M) continue;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int col = col0 + tx * 4 + c;
+      if (col >= N) continue;
+      float v = acc[a][c];
+      if (b) v = v + b[col];
+      if (flags & F_RELU_OUT) v = v > 0.0f ? v : 0.0f;
+      if (flags & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
+      float* y = Y + (int64_t)r * ldy + col;
+      *y = (flags & F_ACCUM) ? *y + v : v;
+    }
+  }
+}
+
+// hk.LayerNorm over the last axis (C ≤ 512): mean, centred variance, eps 1e-5; one wave per row
+__global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ X, int ldx, float* __restrict__ Y,
+                                                   int ldy, int M, int C, const float* __restrict__ s,
+                                                   const float* __restrict__ o) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* x = X + row * ldx;
+  float v[8];
+  const int per = (C + 63) / 64;
+  float sum = 0.0f;
+  for (int i = 0; i < per; ++i) {
+    int c = lane + 64 * i;
+    v[i] = c < C ? x[c] : 0.0f;
+    sum += v[i];
+  }
+  for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
+  const float mean = sum / (float)C;
+  float sq = 0.0f;
+  for (int i = 0; i < per; ++i) {
+    int c = lane + 64 * i;
+    if (c < C) {
+      float d = v[i] - mean;
+      sq += d * d;
+    }
+  }
+  for (int m = 32; m >= 1; m >>= 1) sq += __shfl_xor(sq, m);
+  const float rs = 1.0f / sqrtf(sq / (float)C + 1e-5f);
+  float* y = Y + row * ldy;
+  for (int i = 0; i < per; ++i) {
+    int c = lane + 64 * i;
+    if (c < C) y[c] = (s[c] * rs) * (v[i] - mean) + o[c];
+  }
+}
+
+// y = x / (|x|_2 + 1e-6) (model.py:148-162, "spherical"), 128 channels, one wave per row
+__global__ void k_spherical(float* __restrict__ X, int M) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float* x = X + row * 128;
+  float a = x[lane], b = x[lane + 64];
+  float s = a * a + b * b;
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  const float d = sqrtf(s) + 1e-6f;
+  x[lane] = a / d;
+  x[lane + 64] = b / d;
+}
+
+// codes (FSQ grid, renorm off: digit - L/2) → up_proj → [PE(t; T_pad) | up] rows of `orig_in`
+__global__ void k_up_init(const uint32_t* __restrict__ tokens, int T, const int* __restrict__ levels, int D,
+                          const float* __restrict__ w_up, const float* __restrict__ b_up,
+                          const float* __restrict__ pe_tok, float* __restrict__ orig_in) {
+  const int t = blockIdx.x, c = threadIdx.x;  // 128 threads
+  if (t >= T) return;
+  uint32_t tok = tokens[t];
+  float code[8];
+  uint32_t basis = 1;
+  for (int d = 0; d < D; ++d) {
+    const uint32_t L = (uint32_t)levels[d];
+    const int digit = (int)((tok / basis) % L);
+    code[d] = (float)(digit - (int)(L / 2));
+    basis *= L;
+  }
+  float acc = 0.0f;
+  for (int d = 0; d < D; ++d) acc = __builtin_fmaf(code[d], w_up[d * 128 + c], acc);
+  orig_in[(int64_t)t * 256 + c] = pe_tok[(int64_t)t * 128 + c];
+  orig_in[(int64_t)t * 256 + 128 + c] = acc + b_up[c];
+}
+
+// Upsampler attention, gated (modules.py:271-382): one wave per (node i, head h); all T keys real
+__global__ __launch_bounds__(256) void k_up_attn(const float* __restrict__ q, const float* __restrict__ k,
+                                                 const float* __restrict__ v, const float* __restrict__ gate,
+                                                 float* __restrict__ out, int N, int T) {
+  __shared__ float wsh[4][512];
+  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6;
+  const int i = blockIdx.x;
+  if (i >= N) return;
+  const float* qi = q + (int64_t)i * 128 + h * 32;
+  float l[8];
+  float mx = -INFINITY;
+  for (int s = 0; s < 8; ++s) {
+    int j = lane + 64 * s;
+    float acc = 0.0f;
+    if (j < T) {
+      const float* kj = k + (int64_t)j * 128 + h * 32;
+      for (int c = 0; c < 32; ++c) acc = __builtin_fmaf(qi[c], kj[c], acc);
+    }
+    l[s] = j < T ? acc : -INFINITY;
+    mx = fmaxf(mx, l[s]);
+  }
+  for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
+  float sum = 0.0f;
+  for (int s = 0; s < 8; ++s) {
+    int j = lane + 64 * s;
+    float e = j < T ? expf(l[s] - mx) : 0.0f;
+    l[s] = e;
+    sum += e;
+  }
+  for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
+  for (int s = 0; s < 8; ++s) {
+    int j = lane + 64 * s;
+    if (j < T) wsh[h][j] = l[s] / sum;
+  }
+  __syncthreads();
+  if (lane < 32) {
+    float acc = 0.0f;
+    for (int j = 0; j < T; ++j) acc = __builtin_fmaf(wsh[h][j], v[(int64_t)j * 128 + h * 32 + lane], acc);
+    out[(int64_t)i * 128 + h * 32 + lane] = acc * gate[(int64_t)i * 128 + h * 32 + lane];
+  }
+}
+
+// P[i*N+j][c] = left[i][c] * right[j][c] (256 channels, einsum "nd,kd->nkd")
+__global__ void k_pair_product(const float* __restrict__ left, const float* __restrict__ right, float* __restrict__ P,
+                               int N) {
+  const int64_t pr = blockIdx.x;
+  const int i = (int)(pr / N), j = (int)(pr % N), c = threadIdx.x;
+  P[pr * 256 + c] = left[(int64_t)i * 256 + c] * right[(int64_t)j * 256 + c];
+}
+
+// C[i*N+j] = [PE(j - i; 512) | pair0[i*N+j]] (sequence_decoder.py:69-99)
+__global__ void k_pair_concat(const float* __restrict__ pe_rel /*[1023][128], row = d + 511*/,
+                              const float* __restrict__ pair0, float* __restrict__ C, int N) {
+  const int64_t pr = blockIdx.x;
+  const int i = (int)(pr / N), j = (int)(pr % N), c = threadIdx.x;
+  C[pr * 256 + c] = pe_rel[(int64_t)(j - i + 511) * 128 + c];
+  C[pr * 256 + 128 + c] = pair0[pr * 128 + c];
+}
+
+// ---------------------------------------------------------------- structure module helpers
+__device__ __forceinline__ void quat_to_rot(const float* q, float* r) {
+  // QUAT_TO_ROT contraction (quat_affine.py:43-56, 143-157)
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  r[0] = w * w + x * x - y * y - z * z;
+  r[1] = 2.0f * (x * y) - 2.0f * (w * z);
+  r[2] = 2.0f * (x * z) + 2.0f * (w * y);
+  r[3] = 2.0f * (x * y) + 2.0f * (w * z);
+  r[4] = w * w - x * x + y * y - z * z;
+  r[5] = 2.0f * (y * z) - 2.0f * (w * x);
+  r[6] = 2.0f * (x * z) - 2.0f * (w * y);
+  r[7] = 2.0f * (y * z) + 2.0f * (w * x);
+  r[8] = w * w - x * x - y * y + z * z;
+}
+
+// affine tensor [N][7] (unit quaternion, translation) → rotation [N][9]; identity init
+__global__ void k_affine_init(float* __restrict__ aff, float* __restrict__ rot, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const float a[7] = {1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < 7; ++c) aff[i * 7 + c] = a[c];
+  quat_to_rot(a, rot + i * 9);
+}
+
+// QuatAffine.pre_compose (quat_affine.py:288-317): q += q ⊗ (0, v); t += R·dt; renormalise
+__global__ void k_affine_update(float* __restrict__ aff, float* __restrict__ rot, const float* __restrict__ upd,
+                                int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  float* a = aff + i * 7;
+  float* R = rot + i * 9;
+  const float* u = upd + i * 6;
+  const float q0 = a[0], q1 = a[1], q2 = a[2], q3 = a[3];
+  const float v1 = u[0], v2 = u[1], v3 = u[2];
+  float nq[4];
+  nq[0] = q0 + (-(q1 * v1) - q2 * v2 - q3 * v3);
+  nq[1] = q1 + (q0 * v1 + q2 * v3 - q3 * v2);
+  nq[2] = q2 + (q0 * v2 - q1 * v3 + q3 * v1);
+  nq[3] = q3 + (q0 * v3 + q1 * v2 - q2 * v1);
+  float dt[3];
+  for (int r = 0; r < 3; ++r) dt[r] = R[3 * r] * u[3] + R[3 * r + 1] * u[4] + R[3 * r + 2] * u[5];
+  const float nrm = sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+  for (int c = 0; c < 4; ++c) a[c] = nq[c] / nrm;
+  for (int c = 0; c < 3; ++c) a[4 + c] = a[4 + c] + dt[c];
+  quat_to_rot(a, R);
+}
+
+// IPA points to the global frame (apply_to_point, quat_affine.py): q [N][12][4][3], kv [N][12][12][3]
+__global__ void k_ipa_points(const float* __restrict__ qpl /*[N][144]*/, const float* __restrict__ kvpl /*[N][432]*/,
+                             const float* __restrict__ aff, const float* __restrict__ rot, float* __restrict__ qpg,
+                             float* __restrict__ kvpg, int N) {
+  const int i = blockIdx.x, t = threadIdx.x;  // 192 threads: 48 q points + 144 kv points
+  if (i >= N) return;
+  const float* R = rot + i * 9;
+  const float* tr = aff + i * 7 + 4;
+  float x, y, z;
+  float* dst;
+  if (t < 48) {
+    x = qpl[i * 144 + t];
+    y = qpl[i * 144 + 48 + t];
+    z = qpl[i * 144 + 96 + t];
+    dst = qpg + ((int64_t)i * 48 + t) * 3;
+  } else {
+    const int p = t - 48;
+    x = kvpl[i * 432 + p];
+    y = kvpl[i * 432 + 144 + p];
+    z = kvpl[i * 432 + 288 + p];
+    dst = kvpg + ((int64_t)i * 144 + p) * 3;
+  }
+  for (int r = 0; r < 3; ++r) dst[r] = R[3 * r] * x + R[3 * r + 1] * y + R[3 * r + 2] * z + tr[r];
+}
+
+// Invariant point attention for query residue i (folding.py:69-289): logits over all N residues,
+// softmax, then the 2112 output features [scalar 192 | local points x,y,z 3×96 | norms 96 |
+// pair 1536]. One workgroup per i.
+__global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /*[N][192]*/,
+                                                  const float* __restrict__ kvs /*[N][384]*/,
+                                                  const float* __restrict__ qpg, const float* __restrict__ kvpg,
+                                                  const float* __restrict__ b2d /*[N][N][12], × sqrt(1/3)*/,
+                                                  const float* __restrict__ zln /*[N][N][128]*/,
+                                                  const float* __restrict__ pw /*[12]*/,
+                                                  const float* __restrict__ aff, const float* __restrict__ rot,
+                                                  float* __restrict__ feat /*[N][2112]*/, int N) {
+  __shared__ float att[12][512];
+  __shared__ float res_pt[12 * 8 * 3];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const float sw = 0.144337567297406f;  // sqrt(1 / (3 * 16))
+  // logits
+  for (int e = tid; e < 12 * N; e += 256) {
+    const int h = e / N, j = e - h * N;
+    float sc = 0.0f;
+    const float* q = qs + (int64_t)i * 192 + h * 16;
+    const float* k = kvs + (int64_t)j * 384 + h * 32;
+    for (int c = 0; c < 16; ++c) sc = __builtin_fmaf(sw * q[c], k[c], sc);
+    float pt = 0.0f;
+    for (int p = 0; p < 4; ++p) {
+      const float* qp = qpg + (((int64_t)i * 12 + h) * 4 + p) * 3;
+      const float* kp = kvpg + (((int64_t)j * 12 + h) * 12 + p) * 3;
+      const float dx = qp[0] - kp[0], dy = qp[1] - kp[1], dz = qp[2] - kp[2];
+      const float d2 = (dx * dx + dy * dy) + dz * dz;
+      pt += pw[h] * d2;
+    }
+    att[h][j] = (sc + (-0.5f * pt)) + b2d[((int64_t)i * N + j) * 12 + h];
+  }
+  __syncthreads();
+  // softmax per head (waves 0..3 take heads h, h+4, h+8)
+  {
+    const int lane = tid & 63, w = tid >> 6;
+    for (int h = w; h < 12; h += 4) {
+      float mx = -INFINITY;
+      for (int j = lane; j < N; j += 64) mx = fmaxf(mx, att[h][j]);
+      for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
+      float s = 0.0f;
+      for (int j = lane; j < N; j += 64) {
+        float e = expf(att[h][j] - mx);
+        att[h][j] = e;
+        s += e;
+      }
+      for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+      for (int j = lane; j < N; j += 64) att[h][j] = att[h][j] / s;
+    }
+  }
+  __syncthreads();
+  float* f = feat + (int64_t)i * 2112;
+  // scalar values (192) and global value points (288)
+  for (int o = tid; o < 192 + 288; o += 256) {
+    float acc = 0.0f;
+    if (o < 192) {
+      const int h = o / 16, c = o % 16;
+      for (int j = 0; j < N; ++j) acc = __builtin_fmaf(att[h][j], kvs[(int64_t)j * 384 + h * 32 + 16 + c], acc);
+      f[o] = acc;
+    } else {
+      const int q = o - 192, h = q / 24, p = (q / 3) % 8, xyz = q % 3;
+      for (int j = 0; j < N; ++j)
+        acc = __builtin_fmaf(att[h][j], kvpg[(((int64_t)j * 12 + h) * 12 + 4 + p) * 3 + xyz], acc);
+      res_pt[q] = acc;
+    }
+  }
+  // attention over the pair representation: thread → channel c, heads hg, hg+2, ...
+  {
+    const int c = tid & 127, hg = tid >> 7;
+    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* zr = zln + (int64_t)i * N * 128 + c;
+    for (int j = 0; j < N; ++j) {
+      const float zv = zr[(int64_t)j * 128];
+#pragma unroll
+      for (int u = 0; u < 6; ++u) acc[u] = __builtin_fmaf(att[hg + 2 * u][j], zv, acc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 6; ++u) f[576 + (hg + 2 * u) * 128 + c] = acc[u];
+  }
+  __syncthreads();
+  // global → local frame of i (invert_point) and norms
+  if (tid < 96) {
+    const int h = tid / 8, p = tid % 8;
+    const float* R = rot + i * 9;
+    const float* tr = aff + i * 7 + 4;
+    const float gx = res_pt[(h * 8 + p) * 3 + 0] - tr[0];
+    const float gy = res_pt[(h * 8 + p) * 3 + 1] - tr[1];
+    const float gz = res_pt[(h * 8 + p) * 3 + 2] - tr[2];
+    const float lx = R[0] * gx + R[3] * gy + R[6] * gz;
+    const float ly = R[1] * gx + R[4] * gy + R[7] * gz;
+    const float lz = R[2] * gx + R[5] * gy + R[8] * gz;
+    f[192 + tid] = lx;
+    f[288 + tid] = ly;
+    f[384 + tid] = lz;
+    f[480 + tid] = sqrtf(((1e-8f + lx * lx) + ly * ly) + lz * lz);
+  }
+}
+
+// Backbone torsions → frames → atom14 → atom37 (folding.py:674-746, all_atom.py:473-595, :122-135)
+// plus the trajectory row (affine × [1,1,1,1,10,10,10]).
+__global__ void k_sc_geom(const float* __restrict__ aff, const float* __restrict__ rot,
+                          const float* __restrict__ unnorm /*[N][6]*/, float* __restrict__ angles /*[N][3][2]*/,
+                          float* __restrict__ traj /*[N][7]*/, float* __restrict__ atom37 /*[N][37][3] or null*/,
+                          float* __restrict__ atom14 /*[N][14][3] or null*/, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const float* a = aff + i * 7;
+  const float* R = rot + i * 9;
+  float sn[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {1.f, 1.f, 1.f, 1.f};
+  for (int t = 0; t < 3; ++t) {
+    const float s = unnorm[i * 6 + 2 * t], c = unnorm[i * 6 + 2 * t + 1];
+    const float d = sqrtf(fmaxf(s * s + c * c, 1e-12f));
+    sn[t + 1] = s / d;
+    cs[t + 1] = c / d;
+    angles[(i * 3 + t) * 2 + 0] = sn[t + 1];
+    angles[(i * 3 + t) * 2 + 1] = cs[t + 1];
+  }
+  for (int c = 0; c < 4; ++c) traj[i * 7 + c] = a[c];
+  for (int c = 0; c < 3; ++c) traj[i * 7 + 4 + c] = a[4 + c] * 10.0f;
+  if (!atom37 && !atom14) return;
+  const float T0[3] = {a[4] * 10.0f, a[5] * 10.0f, a[6] * 10.0f};  // scale_translation(position_scale)
+  float fr[4][12];  // per group: rot (9, row-major) + trans (3), to global
+  for (int g = 0; g < 4; ++g) {
+    // default frame ∘ rotation about x by torsion g (group 0: identity rotation)
+    float m[9], mt[3];
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c) m[3 * r + c] = kDefaultFrame[g][r][c];
+      mt[r] = kDefaultFrame[g][r][3];
+    }
+    const float rx[9] = {1.f, 0.f, 0.f, 0.f, cs[g], -sn[g], 0.f, sn[g], cs[g]};
+    float mb[9];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) mb[3 * r + c] = m[3 * r] * rx[c] + m[3 * r + 1] * rx[3 + c] + m[3 * r + 2] * rx[6 + c];
+    // backbone-to-global ∘ frame-to-backbone
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c)
+        fr[g][3 * r + c] = R[3 * r] * mb[c] + R[3 * r + 1] * mb[3 + c] + R[3 * r + 2] * mb[6 + c];
+      fr[g][9 + r] = (R[3 * r] * mt[0] + R[3 * r + 1] * mt[1] + R[3 * r + 2] * mt[2]) + T0[r];
+    }
+  }
+  float p14[14][3];
+  for (int at = 0; at < 14; ++at) {
+    const float* F = fr[kAtom14Group[at]];
+    for (int r = 0; r < 3; ++r) {
+      const float v = F[3 * r] * kAtom14Pos[at][0] + F[3 * r + 1] * kAtom14Pos[at][1] + F[3 * r + 2] * kAtom14Pos[at][2] +
+                      F[9 + r];
+      p14[at][r] = v * kAtom14Mask[at];
+    }
+  }
+  if (atom14)
+    for (int at = 0; at < 14; ++at)
+      for (int r = 0; r < 3; ++r) atom14[(i * 14 + at) * 3 + r] = p14[at][r];
+  if (atom37) {
+    // atom14_to_atom37 for the dummy ALA aatype, then × atom37_gt_exists (N, CA, C, O)
+    for (int at = 0; at < 37; ++at) {
+      const float gt = (at == 0 || at == 1 || at == 2 || at == 4) ? 1.0f : 0.0f;
+      for (int r = 0; r < 3; ++r) atom37[(i * 37 + at) * 3 + r] = (p14[kAla37To14[at]][r] * kAla37Mask[at]) * gt;
+    }
+  }
+}
+
+}  // namespace dec
+}  // namespace pst
+
+// ======================================================================== host side / C ABI
+using namespace pst::dec;
+
+namespace {
+
+struct Lin {
+  const float* w = nullptr;
+  const float* b = nullptr;
+  int in = 0, out = 0;
+};
+struct LnP {
+  const float* s = nullptr;
+  const float* o = nullptr;
+};
+
+struct DecWeights {
+  Lin up_proj;
+  // upsampler block b: norms and attention weights are [3][...] stacked
+  LnP qn[3], dn[3];
+  const float *wq[3], *wk[3], *wv[3], *wg[3], *gb[3], *wo[3], *ob[3];
+  LnP rt_ln[3], ot_ln[3];
+  Lin rt1[3], rt2[3], ot1[3], ot2[3];
+  Lin proj_original;
+  Lin seq_linear;
+  LnP pt_ln;
+  Lin pt1, pt2;
+  LnP pr_ln_in, pr_ln_out;
+  Lin left, right, right1, out1, out2;
+  Lin affine_update;
+  LnP att_ln;
+  const float* tpw;
+  Lin att2d, kv_point, kv_scalar, out_proj, q_point, q_scalar;
+  Lin sc_in, sc_in1, rb1, rb1_1, rb2, rb2_1, angles;
+  Lin tr[3];
+  LnP tr_ln;
+  Lin init_proj;
+  LnP pair_ln, single_ln;
+};
+
+}  // namespace
+
+struct pst_decoder {
+  int device = 0;
+  pst_model_desc desc{};
+  int D = 6, df = 1;
+  hipStream_t stream = nullptr;
+  std::string err;
+  float* d_blob = nullptr;
+  int* d_levels = nullptr;
+  float* d_pe_node = nullptr;  // PE(i; 512) [512][128]
+  float* d_pe_tok = nullptr;   // PE(t; 512/df) [512/df][128]
+  float* d_pe_rel = nullptr;   // PE(d; 512), d = -511..511 [1023][128]
+  float* d_pw = nullptr;       // IPA point weights [12]
+  DecWeights W{};
+  // scratch (grow-only, sized for N = 512)
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  // last call's intermediates (per protein offsets) for pst_decoder_debug
+  std::vector<float> last_single, last_pair, last_traj, last_angles, last_atom14;
+};
+
+namespace {
+
+std::string g_dec_create_error;
+
+#define DCHK(x)                                                               \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      dec->err = std::string(#x) + ": " + hipGetErrorString(e_);              \
+      return PST_E_HIP;                                                       \
+    }                                                                         \
+  } while (0)
+
+int dfail(pst_decoder* dec, int code, const std::string& m) {
+  dec->err = m;
+  return code;
+}
+
+// walk the decoder-half blob in pst_amd.params.decoder_param_spec order
+size_t walk_decoder(const float* base, int D, DecWeights* W) {
+  size_t o = 0;
+  auto take = [&](size_t n) {
+    const float* p = base ? base + o : nullptr;
+    o += n;
+    return p;
+  };
+  auto lin = [&](Lin& l, int in, int out) {
+    l.in = in;
+    l.out = out;
+    l.w = take((size_t)in * out);
+    l.b = take(out);
+  };
+  const int H = 128;
+  lin(W->up_proj, D, H);
+  // _scaler_spec(US/cross_attn_scaler_iteration, 3)
+  const float *qs = take(3 * H), *qo = take(3 * H), *ds = take(3 * H), *dso = take(3 * H);
+  const float *wq = take(3 * H * H), *wk = take(3 * H * H), *wv = take(3 * H * H), *wg = take(3 * H * H);
+  const float *gb = take(3 * H), *wo = take(3 * H * H), *ob = take(3 * H);
+  const float *rls = take(3 * H), *rlo = take(3 * H), *r1w = take(3 * H * 2 * H), *r1b = take(3 * 2 * H);
+  const float *r2w = take(3 * 2 * H * H), *r2b = take(3 * H);
+  const float *ols = take(3 * H), *olo = take(3 * H), *o1w = take(3 * H * 2 * H), *o1b = take(3 * 2 * H);
+  const float *o2w = take(3 * 2 * H * H), *o2b = take(3 * H);
+  if (base)
+    for (int b = 0; b < 3; ++b) {
+      W->qn[b] = {qs + b * H, qo + b * H};
+      W->dn[b] = {ds + b * H, dso + b * H};
+      W->wq[b] = wq + (size_t)b * H * H;
+      W->wk[b] = wk + (size_t)b * H * H;
+      W->wv[b] = wv + (size_t)b * H * H;
+      W->wg[b] = wg + (size_t)b * H * H;
+      W->gb[b] = gb + b * H;
+      W->wo[b] = wo + (size_t)b * H * H;
+      W->ob[b] = ob + b * H;
+      W->rt_ln[b] = {rls + b * H, rlo + b * H};
+      W->rt1[b] = {r1w + (size_t)b * H * 2 * H, r1b + b * 2 * H, H, 2 * H};
+      W->rt2[b] = {r2w + (size_t)b * 2 * H * H, r2b + b * H, 2 * H, H};
+      W->ot_ln[b] = {ols + b * H, olo + b * H};
+      W->ot1[b] = {o1w + (size_t)b * H * 2 * H, o1b + b * 2 * H, H, 2 * H};
+      W->ot2[b] = {o2w + (size_t)b * 2 * H * H, o2b + b * H, 2 * H, H};
+    }
+  lin(W->proj_original, 2 * H, H);
+  lin(W->seq_linear, 2 * H, H);
+  W->pt_ln = {take(H), take(H)};
+  lin(W->pt1, H, 2 * H);
+  lin(W->pt2, 2 * H, H);
+  W->pr_ln_in = {take(H), take(H)};
+  W->pr_ln_out = {take(H), take(H)};
+  lin(W->left, H, 2 * H);
+  lin(W->right, H, 2 * H);
+  lin(W->right1, 2 * H, H);
+  lin(W->out1, 2 * H, 2 * H);
+  lin(W->out2, 2 * H, H);
+  const int S = 384;
+  lin(W->affine_update, S, 6);
+  W->att_ln = {take(S), take(S)};
+  W->tpw = take(12);
+  lin(W->att2d, H, 12);
+  lin(W->kv_point, S, 432);
+  lin(W->kv_scalar, S, S);
+  lin(W->out_proj, 2112, S);
+  lin(W->q_point, S, 144);
+  lin(W->q_scalar, S, 192);
+  lin(W->sc_in, S, H);
+  lin(W->sc_in1, H, H);
+  lin(W->rb1, H, H);
+  lin(W->rb1_1, H, H);
+  lin(W->rb2, H, H);
+  lin(W->rb2_1, H, H);
+  lin(W->angles, H, 6);
+  for (int t = 0; t < 3; ++t) lin(W->tr[t], S, S);
+  W->tr_ln = {take(S), take(S)};
+  lin(W->init_proj, H, S);
+  W->pair_ln = {take(H), take(H)};
+  W->single_ln = {take(H), take(H)};
+  return o;
+}
+
+// scaled-grid launcher helpers
+inline void gemm(hipStream_t st, const float* X, int ldx, const Lin& L, float* Y, int ldy, int M, int flags,
+                 const float* b_override = nullptr, bool use_bias = true) {
+  dim3 grid((L.out + 63) / 64, (M + 63) / 64);
+  hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, st, X, ldx, L.w, L.out, use_bias ? (b_override ? b_override : L.b) : nullptr,
+                     Y, ldy, M, L.out, L.in, flags);
+}
+inline void gemm_raw(hipStream_t st, const float* X, int ldx, const float* Wt, int K, int N, const float* b, float* Y,
+                     int ldy, int M, int flags) {
+  dim3 grid((N + 63) / 64, (M + 63) / 64);
+  hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, st, X, ldx, Wt, N, b, Y, ldy, M, N, K, flags);
+}
+inline void layernorm(hipStream_t st, const float* X, int ldx, float* Y, int ldy, int M, int C, const LnP& p) {
+  hipLaunchKernelGGL(k_layernorm, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, Y, ldy, M, C, p.s, p.o);
+}
+
+struct Scratch {
+  float *orig_in, *orig, *res, *ln_a, *ln_b, *q, *k, *v, *gate, *wavg, *tr_h;
+  float *left, *right, *P, *h1, *pair0, *catb, *lin_out, *lnz, *z, *zln, *b2d;
+  float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
+  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14;
+};
+
+int ensure_ws(pst_decoder* dec, Scratch* S) {
+  const size_t NN = 512, NP = NN * NN;
+  struct It {
+    float** p;
+    size_t n;
+  };
+  It items[] = {{&S->orig_in, NN * 256}, {&S->orig, NN * 128},   {&S->res, NN * 128},    {&S->ln_a, NN * 128},
+                {&S->ln_b, NN * 128},    {&S->q, NN * 128},      {&S->k, NN * 128},      {&S->v, NN * 128},
+                {&S->gate, NN * 128},    {&S->wavg, NN * 128},   {&S->tr_h, NN * 256},   {&S->left, NN * 256},
+                {&S->right, NN * 256},   {&S->P, NP * 256},      {&S->h1, NP * 256},     {&S->pair0, NP * 128},
+                {&S->catb, NP * 256},    {&S->lin_out, NP * 128}, {&S->lnz, NP * 128},   {&S->z, NP * 128},
+                {&S->zln, NP * 128},     {&S->b2d, NP * 12},     {&S->single_ln, NN * 128}, {&S->act, NN * 384},
+                {&S->init_act, NN * 128}, {&S->act_ln, NN * 384}, {&S->tmp384a, NN * 384}, {&S->tmp384b, NN * 384},
+                {&S->qs, NN * 192},      {&S->kvs, NN * 384},    {&S->qpl, NN * 144},    {&S->kvpl, NN * 432},
+                {&S->qpg, NN * 144},     {&S->kvpg, NN * 432},   {&S->feat, NN * 2112},  {&S->upd, NN * 6},
+                {&S->aff, NN * 7},       {&S->rot, NN * 9},      {&S->sca, NN * 128},    {&S->scb, NN * 128},
+                {&S->sct, NN * 128},     {&S->unnorm, NN * 6},   {&S->angles, 8 * NN * 6}, {&S->traj, 8 * NN * 7},
+                {&S->atom37, NN * 111},  {&S->atom14, NN * 42}};
+  size_t total = 0;
+  for (auto& it : items) total += (it.n * sizeof(float) + 255) / 256 * 256;
+  if (!dec->ws) {
+    hipError_t e = hipMalloc(&dec->ws, total);
+    if (e != hipSuccess) return dfail(dec, PST_E_NOMEM, std::string("decoder workspace: ") + hipGetErrorString(e));
+    dec->ws_bytes = total;
+  }
+  char* p = (char*)dec->ws;
+  for (auto& it : items) {
+    *it.p = (float*)p;
+    p += (it.n * sizeof(float) + 255) / 256 * 256;
+  }
+  return PST_OK;
+}
+
+// decode one protein: tokens (device, T) → atom37 [N][37][3] (device), N = df·T
+int decode_one(pst_decoder* dec, Scratch& S, const uint32_t* d_tok, int T, bool keep_debug) {
+  const DecWeights& W = dec->W;
+  hipStream_t st = dec->stream;
+  const int N = T * dec->df;
+  if (T <= 0) return PST_OK;
+  // ---- upsampler (CrossAttentionScaler, use_original_posenc)
+  hipLaunchKernelGGL(k_up_init, dim3(T), dim3(128), 0, st, d_tok, T, dec->d_levels, dec->D, W.up_proj.w, W.up_proj.b,
+                     dec->d_pe_tok, S.orig_in);
+  gemm(st, S.orig_in, 256, W.proj_original, S.orig, 128, T, 0);
+  DCHK(hipMemcpyAsync(S.res, dec->d_pe_node, sizeof(float) * N * 128, hipMemcpyDeviceToDevice, st));
+  for (int b = 0; b < 3; ++b) {
+    layernorm(st, S.res, 128, S.ln_a, 128, N, 128, W.qn[b]);
+    layernorm(st, S.orig, 128, S.ln_b, 128, T, 128, W.dn[b]);
+    gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, N, 0);
+    gemm_raw(st, S.ln_a, 128, W.wg[b], 128, 128, W.gb[b], S.gate, 128, N, F_SIGMOID_OUT);
+    gemm_raw(st, S.ln_b, 128, W.wk[b], 128, 128, nullptr, S.k, 128, T, 0);
+    gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, T, 0);
+    // q · key_dim^-0.5 folded into the attention kernel's operand: scale q in place
+    hipLaunchKernelGGL(k_scale, dim3((N * 128 + 255) / 256), dim3(256), 0, st, S.q, N * 128, 0.176776695296637f);
+    hipLaunchKernelGGL(k_up_attn, dim3(N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, N, T);
+    gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, N, F_ACCUM);
+    // resampled transition (residual)
+    layernorm(st, S.res, 128, S.ln_a, 128, N, 128, W.rt_ln[b]);
+    gemm(st, S.ln_a, 128, W.rt1[b], S.tr_h, 256, N, F_RELU_OUT);
+    gemm(st, S.tr_h, 256, W.rt2[b], S.res, 128, N, F_ACCUM);
+    // original transition (residual)
+    layernorm(st, S.orig, 128, S.ln_b, 128, T, 128, W.ot_ln[b]);
+    gemm(st, S.ln_b, 128, W.ot1[b], S.tr_h, 256, T, F_RELU_OUT);
+    gemm(st, S.tr_h, 256, W.ot2[b], S.orig, 128, T, F_ACCUM);
+  }
+  hipLaunchKernelGGL(k_spherical, dim3((N + 3) / 4), dim3(256), 0, st, S.res, N);  // s_i
+  // ---- sequence decoder: pair representation
+  const int NP = N * N;
+  layernorm(st, S.res, 128, S.ln_a, 128, N, 128, W.pr_ln_in);
+  gemm(st, S.ln_a, 128, W.left, S.left, 256, N, 0);
+  gemm(st, S.ln_a, 128, W.right, S.right, 256, N, 0);
+  hipLaunchKernelGGL(k_pair_product, dim3(NP), dim3(256), 0, st, S.left, S.right, S.P, N);
+  gemm(st, S.P, 256, W.out1, S.h1, 256, NP, F_RELU_OUT);
+  gemm(st, S.h1, 256, W.out2, S.pair0, 128, NP, 0);
+  gemm(st, S.P, 256, W.right1, S.lin_out, 128, NP, 0);
+  hipLaunchKernelGGL(k_add, dim3((NP * 128 + 255) / 256), dim3(256), 0, st, S.pair0, S.lin_out, (int64_t)NP * 128);
+  layernorm(st, S.pair0, 128, S.pair0, 128, NP, 128, W.pr_ln_out);
+  hipLaunchKernelGGL(k_pair_concat, dim3(NP), dim3(128), 0, st, dec->d_pe_rel, S.pair0, S.catb, N);
+  gemm(st, S.catb, 256, W.seq_linear, S.lin_out, 128, NP, 0);
+  layernorm(st, S.lin_out, 128, S.lnz, 128, NP, 128, W.pt_ln);
+  gemm(st, S.lnz, 128, W.pt1, S.h1, 256, NP, F_RELU_OUT);
+  gemm(st, S.h1, 256, W.pt2, S.z, 128, NP, 0);  // z_ij (Transition output, no residual)
+  // ---- structure module
+  layernorm(st, S.res, 128, S.init_act, 128, N, 128, W.single_ln);
+  gemm(st, S.init_act, 128, W.init_proj, S.act, 384, N, 0);
+  layernorm(st, S.z, 128, S.zln, 128, NP, 128, W.pair_ln);
+  gemm(st, S.zln, 128, W.att2d, S.b2d, 12, NP, 0);
+  hipLaunchKernelGGL(k_scale, dim3((NP * 12 + 255) / 256), dim3(256), 0, st, S.b2d, NP * 12, 0.577350269189626f);
+  hipLaunchKernelGGL(k_affine_init, dim3((N + 63) / 64), dim3(64), 0, st, S.aff, S.rot, N);
+  for (int it = 0; it < 8; ++it) {
+    gemm(st, S.act, 384, W.q_scalar, S.qs, 192, N, 0);
+    gemm(st, S.act, 384, W.kv_scalar, S.kvs, 384, N, 0);
+    gemm(st, S.act, 384, W.q_point, S.qpl, 144, N, 0);
+    gemm(st, S.act, 384, W.kv_point, S.kvpl, 432, N, 0);
+    hipLaunchKernelGGL(k_ipa_points, dim3(N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg, N);
+    hipLaunchKernelGGL(k_ipa_attn, dim3(N), dim3(256), 0, st, S.qs, S.kvs, S.qpg, S.kvpg, S.b2d, S.zln, dec->d_pw,
+                       S.aff, S.rot, S.feat, N);
+    gemm(st, S.feat, 2112, W.out_proj, S.act, 384, N, F_ACCUM);  // act += IPA
+    layernorm(st, S.act, 384, S.act, 384, N, 384, W.att_ln);
+    gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, N, F_RELU_OUT);
+    gemm(st, S.tmp384a, 384, W.tr[1], S.tmp384b, 384, N, F_RELU_OUT);
+    gemm(st, S.tmp384b, 384, W.tr[2], S.act, 384, N, F_ACCUM);  // += input_act
+    layernorm(st, S.act, 384, S.act, 384, N, 384, W.tr_ln);
+    gemm(st, S.act, 384, W.affine_update, S.upd, 6, N, 0);
+    hipLaunchKernelGGL(k_affine_update, dim3((N + 63) / 64), dim3(64), 0, st, S.aff, S.rot, S.upd, N);
+    // MultiRigidSidechain: (0 + Lin(relu(act))) + Lin(relu(initial_act)), 2 residual blocks, angles
+    hipLaunchKernelGGL(k_zero, dim3((N * 128 + 255) / 256), dim3(256), 0, st, S.sca, N * 128);
+    gemm(st, S.act, 384, W.sc_in, S.sca, 128, N, F_RELU_IN | F_ACCUM);
+    gemm(st, S.init_act, 128, W.sc_in1, S.sca, 128, N, F_RELU_IN | F_ACCUM);
+    gemm(st, S.sca, 128, W.rb1, S.scb, 128, N, F_RELU_IN);
+    gemm(st, S.scb, 128, W.rb2, S.sca, 128, N, F_RELU_IN | F_ACCUM);
+    gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, N, F_RELU_IN);
+    gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, N, F_RELU_IN | F_ACCUM);
+    gemm(st, S.sca, 128, W.angles, S.unnorm, 6, N, F_RELU_IN);
+    const bool last = it == 7;
+    hipLaunchKernelGGL(k_sc_geom, dim3((N + 63) / 64), dim3(64), 0, st, S.aff, S.rot, S.unnorm, S.angles + it * 512 * 6,
+                       S.traj + it * 512 * 7, last ? S.atom37 : nullptr, last ? S.atom14 : nullptr, N);
+  }
+  DCHK(hipGetLastError());
+  if (keep_debug) {
+    const size_t o1 = dec->last_single.size();
+    dec->last_single.resize(o1 + (size_t)N * 128);
+    DCHK(hipMemcpyAsync(dec->last_single.data() + o1, S.res, sizeof(float) * N * 128, hipMemcpyDeviceToHost, st));
+    const size_t o2 = dec->last_pair.size();
+    dec->last_pair.resize(o2 + (size_t)NP * 128);
+    DCHK(hipMemcpyAsync(dec->last_pair.data() + o2, S.z, sizeof(float) * NP * 128, hipMemcpyDeviceToHost, st));
+    const size_t o3 = dec->last_traj.size();
+    dec->last_traj.resize(o3 + (size_t)8 * N * 7);
+    for (int it = 0; it < 8; ++it)
+      DCHK(hipMemcpyAsync(dec->last_traj.data() + o3 + (size_t)it * N * 7, S.traj + it * 512 * 7, sizeof(float) * N * 7,
+                          hipMemcpyDeviceToHost, st));
+    const size_t o4 = dec->last_angles.size();
+    dec->last_angles.resize(o4 + (size_t)8 * N * 6);
+    for (int it = 0; it < 8; ++it)
+      DCHK(hipMemcpyAsync(dec->last_angles.data() + o4 + (size_t)it * N * 6, S.angles + it * 512 * 6,
+                          sizeof(float) * N * 6, hipMemcpyDeviceToHost, st));
+    const size_t o5 = dec->last_atom14.size();
+    dec->last_atom14.resize(o5 + (size_t)N * 42);
+    DCHK(hipMemcpyAsync(dec->last_atom14.data() + o5, S.atom14, sizeof(float) * N * 42, hipMemcpyDeviceToHost, st));
+    DCHK(hipStreamSynchronize(st));
+  }
+  return PST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t pst_decoder_param_count(int32_t n_levels) {
+  DecWeights W;
+  return walk_decoder(nullptr, n_levels, &W);
+}
+
+const char* pst_decoder_create_error(void) { return g_dec_create_error.c_str(); }
+
+int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* params, size_t n_params,
+                       pst_decoder** out) {
+  g_dec_create_error.clear();
+  if (!desc || !params || !out) {
+    g_dec_create_error = "null argument";
+    return PST_E_INVALID;
+  }
+  const int D = desc->n_levels, df = desc->downsampling_ratio;
+  if (desc->abi_version != PST_ABI_VERSION || D < 1 || D > 8 || (df != 1 && df != 2 && df != 4) ||
+      desc->seq_max_size != 512) {
+    g_dec_create_error = "unsupported model description";
+    return PST_E_INVALID;
+  }
+  if (n_params != pst_decoder_param_count(D)) {
+    g_dec_create_error = "decoder blob has " + std::to_string(n_params) + " floats, expected " +
+                         std::to_string(pst_decoder_param_count(D));
+    return PST_E_INVALID;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    g_dec_create_error = "no such HIP device: " + std::to_string(device);
+    return PST_E_HIP;
+  }
+  pst_decoder* dec = new pst_decoder();
+  dec->device = device;
+  dec->desc = *desc;
+  dec->D = D;
+  dec->df = df;
+  auto bad = [&](const char* what) {
+    g_dec_create_error = what;
+    pst_decoder_destroy(dec);
+    return PST_E_HIP;
+  };
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&dec->stream, hipStreamNonBlocking) != hipSuccess)
+    return bad("hip stream creation failed");
+  if (hipMalloc(&dec->d_blob, n_params * sizeof(float)) != hipSuccess ||
+      hipMemcpy(dec->d_blob, params, n_params * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+    return bad("decoder weight upload failed");
+  walk_decoder(dec->d_blob, D, &dec->W);
+  // host-side constants: PE tables, levels, IPA point weights
+  auto up = [&](float** d, const std::vector<float>& h) {
+    return hipMalloc(d, h.size() * sizeof(float)) == hipSuccess &&
+           hipMemcpy(*d, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up(&dec->d_pe_node, pst::pe_rows(0, 512, 512)) || !up(&dec->d_pe_tok, pst::pe_rows(0, 512 / df, 512 / df)) ||
+      !up(&dec->d_pe_rel, pst::pe_rows(-511, 1023, 512)))
+    return bad("PE table upload failed");
+  if (hipMalloc(&dec->d_levels, 8 * sizeof(int)) != hipSuccess ||
+      hipMemcpy(dec->d_levels, desc->levels, 8 * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+    return bad("levels upload failed");
+  {
+    // point_weights = sqrt(1 / (3 · 4 · 9/2)) · softplus(trainable_point_weights)   (folding.py:178-197)
+    DecWeights Wh;
+    walk_decoder(params, D, &Wh);
+    std::vector<float> pw(12);
+    const float base = (float)std::sqrt(1.0 / (3.0 * 4.0 * 9.0 / 2.0));
+    for (int h = 0; h < 12; ++h) {
+      const double x = Wh.tpw[h];
+      const float sp = (float)(x > 20.0 ? x : std::log1p(std::exp(x)));
+      pw[h] = base * sp;
+    }
+    if (!up(&dec->d_pw, pw)) return bad("point weight upload failed");
+  }
+  *out = dec;
+  return PST_OK;
+}
+
+int pst_decoder_destroy(pst_decoder* dec) {
+  if (!dec) return PST_OK;
+  (void)hipSetDevice(dec->device);
+  if (dec->stream) (void)hipStreamSynchronize(dec->stream);
+  for (void* p : {(void*)dec->d_blob, (void*)dec->d_levels, (void*)dec->d_pe_node, (void*)dec->d_pe_tok,
+                  (void*)dec->d_pe_rel, (void*)dec->d_pw, dec->ws})
+    if (p) (void)hipFree(p);
+  if (dec->stream) (void)hipStreamDestroy(dec->stream);
+  delete dec;
+  return PST_OK;
+}
+
+const char* pst_decoder_last_error(const pst_decoder* dec) { return dec ? dec->err.c_str() : "null decoder"; }
+
+int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* token_offsets, int32_t n_prot,
+                       float* atom37_out, int32_t* n_nodes_out) {
+  if (!dec) return PST_E_INVALID;
+  dec->err.clear();
+  if (!tokens || !token_offsets || n_prot < 1 || !atom37_out) return dfail(dec, PST_E_INVALID, "null argument");
+  const int64_t max_tok = 512 / dec->df;
+  int64_t K = 1;
+  for (int d = 0; d < dec->D; ++d) K *= dec->desc.levels[d];
+  for (int b = 0; b < n_prot; ++b) {
+    const int64_t T = token_offsets[b + 1] - token_offsets[b];
+    if (T < 0 || T > max_tok)
+      return dfail(dec, PST_E_INVALID, "protein " + std::to_string(b) + ": token count outside [0, " +
+                                           std::to_string(max_tok) + "]");
+    for (int64_t t = token_offsets[b]; t < token_offsets[b + 1]; ++t)
+      if ((int64_t)tokens[t] >= K) return dfail(dec, PST_E_INVALID, "token id out of range for the codebook");
+  }
+  DCHK(hipSetDevice(dec->device));
+  Scratch S;
+  int rc = ensure_ws(dec, &S);
+  if (rc) return rc;
+  const bool keep = getenv("PST_DEBUG") && getenv("PST_DEBUG")[0] == '1';
+  dec->last_single.clear();
+  dec->last_pair.clear();
+  dec->last_traj.clear();
+  dec->last_angles.clear();
+  dec->last_atom14.clear();
+  uint32_t* d_tok = nullptr;
+  DCHK(hipMalloc(&d_tok, sizeof(uint32_t) * 512));
+  int64_t node_off = 0;
+  for (int b = 0; b < n_prot; ++b) {
+    const int T = (int)(token_offsets[b + 1] - token_offsets[b]);
+    const int N = T * dec->df;
+    if (T > 0) {
+      hipError_t e = hipMemcpyAsync(d_tok, tokens + token_offsets[b], sizeof(uint32_t) * T, hipMemcpyHostToDevice,
+                                    dec->stream);
+      if (e == hipSuccess) rc = decode_one(dec, S, d_tok, T, keep);
+      else rc = dfail(dec, PST_E_HIP, hipGetErrorString(e));
+      if (rc == PST_OK) {
+        e = hipMemcpyAsync(atom37_out + node_off * 111, S.atom37, sizeof(float) * N * 111, hipMemcpyDeviceToHost,
+                           dec->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(dec->stream);
+        if (e != hipSuccess) rc = dfail(dec, PST_E_HIP, hipGetErrorString(e));
+      }
+      if (rc) break;
+    }
+    if (n_nodes_out) n_nodes_out[b] = N;
+    node_off += N;
+  }
+  (void)hipFree(d_tok);
+  return rc;
+}
+
+int pst_decoder_debug(pst_decoder* dec, int32_t which, float* out, size_t n_floats) {
+  if (!dec || !out) return PST_E_INVALID;
+  const std::vector<float>* v = which == 0 ? &dec->last_single
+                                : which == 1 ? &dec->last_pair
+                                : which == 2 ? &dec->last_traj
+                                : which == 3 ? &dec->last_angles
+                                : which == 4 ? &dec->last_atom14
+                                             : nullptr;
+  if (!v) return dfail(dec, PST_E_INVALID, "unknown debug id");
+  if (v->empty()) return dfail(dec, PST_E_INVALID, "no intermediates kept (set PST_DEBUG=1)");
+  if (n_floats < v->size()) return dfail(dec, PST_E_INVALID, "debug buffer too small");
+  std::copy(v->begin(), v->end(), out);
+  return PST_OK;
+}
+
+}  // extern "C"

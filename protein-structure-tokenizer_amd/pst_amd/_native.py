@@ -37,7 +37,9 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_tokenize", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
            "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing", "pst_device_count",
            "pst_codebook_aux_device", "pst_pdb_parse_files", "pst_pdb_parse_strings",
-           "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free")
+           "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free",
+           "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
+           "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_debug")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -90,6 +92,15 @@ def lib():
         L.pst_pdb_batch_error.restype = ctypes.c_char_p
         L.pst_pdb_batch_error.argtypes = [P, ctypes.c_int32]
         L.pst_pdb_batch_free.argtypes = [P]
+        L.pst_decoder_param_count.restype = ctypes.c_size_t
+        L.pst_decoder_param_count.argtypes = [ctypes.c_int32]
+        L.pst_decoder_create.argtypes = [ctypes.c_int32, ctypes.POINTER(_ModelDesc), P, ctypes.c_size_t, ctypes.POINTER(P)]
+        L.pst_decoder_destroy.argtypes = [P]
+        L.pst_decoder_last_error.restype = ctypes.c_char_p
+        L.pst_decoder_last_error.argtypes = [P]
+        L.pst_decoder_create_error.restype = ctypes.c_char_p
+        L.pst_decoder_decode.argtypes = [P, P, P, ctypes.c_int32, P, P]
+        L.pst_decoder_debug.argtypes = [P, ctypes.c_int32, P, ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -306,4 +317,66 @@ class Tokenizer:
         else:
             raise ValueError(which)
         self._check(lib().pst_debug_fetch(self._h, which, _ptr(out), out.nbytes))
+        return out
+
+
+class Decoder:
+    """One libpst decoder context (one GPU): token ids → backbone atom37 coordinates."""
+
+    def __init__(self, device: int = 0, codebook_size: int = 4096, downsampling_ratio: int = 1,
+                 params_blob: Optional[np.ndarray] = None, levels: Optional[Sequence[int]] = None):
+        L = lib()
+        self.levels = tuple(levels or LEVELS[codebook_size])
+        self.D = len(self.levels)
+        self.df = downsampling_ratio
+        self.codebook_size = int(np.prod(self.levels))
+        if params_blob is None:
+            params_blob = _params.pack_decoder(_params.random_full_params(self.D, 0), self.D)
+        self.blob = np.ascontiguousarray(params_blob, dtype=np.float32)
+        n = L.pst_decoder_param_count(self.D)
+        if self.blob.size != n:
+            raise ValueError(f"decoder blob has {self.blob.size} floats, expected {n}")
+        desc = _ModelDesc(ABI_VERSION, self.codebook_size, downsampling_ratio, self.D,
+                          (ctypes.c_int32 * 8)(*(list(self.levels) + [0] * (8 - self.D))), 512, 50)
+        h = ctypes.c_void_p()
+        rc = L.pst_decoder_create(device, ctypes.byref(desc), _ptr(self.blob), self.blob.size, ctypes.byref(h))
+        if rc != PST_OK:
+            raise_for(rc, L.pst_decoder_create_error().decode())
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pst_decoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != PST_OK:
+            raise_for(rc, lib().pst_decoder_last_error(self._h).decode())
+
+    def decode(self, token_lists: Sequence[np.ndarray]) -> List[np.ndarray]:
+        """List of token-id arrays → list of atom37 position arrays [df·T, 37, 3] float32."""
+        toks = [np.asarray(t, np.uint32).reshape(-1) for t in token_lists]
+        off = np.zeros(len(toks) + 1, np.int64)
+        off[1:] = np.cumsum([t.size for t in toks])
+        flat = np.ascontiguousarray(np.concatenate(toks) if toks else np.zeros(0, np.uint32), np.uint32)
+        n_nodes = int(off[-1]) * self.df
+        out = np.zeros((max(n_nodes, 1), 37, 3), np.float32)
+        nn = np.zeros(len(toks), np.int32)
+        self._check(lib().pst_decoder_decode(self._h, _ptr(flat if flat.size else np.zeros(1, np.uint32)), _ptr(off),
+                                             len(toks), _ptr(out), _ptr(nn)))
+        res, o = [], 0
+        for n in nn:
+            res.append(out[o:o + n].copy())
+            o += int(n)
+        return res
+
+    def debug(self, which: int, n_floats: int) -> np.ndarray:
+        out = np.zeros(n_floats, np.float32)
+        self._check(lib().pst_decoder_debug(self._h, which, _ptr(out), n_floats))
         return out

@@ -119,6 +119,25 @@ def full_param_spec(codes_dim: int = 6) -> List[Tuple[str, str, Tuple[int, ...]]
     return sorted(s, key=lambda t: (t[0], t[1]))
 
 
+def decoder_param_count(codes_dim: int = 6) -> int:
+    return int(sum(np.prod(sh) for _, _, sh in decoder_param_spec(codes_dim)))
+
+
+def pack_decoder(params: Dict[str, Dict[str, np.ndarray]], codes_dim: int = 6) -> np.ndarray:
+    """Decoder-half tensors → contiguous float32 blob in `decoder_param_spec` order
+    (the layout `pst_decoder_create` takes)."""
+    parts = []
+    for mod, name, shape in decoder_param_spec(codes_dim):
+        try:
+            a = np.asarray(params[mod][name], dtype=np.float32)
+        except KeyError as e:
+            raise KeyError(f"missing parameter {mod}/{name}") from e
+        if a.shape != shape:
+            raise ValueError(f"{mod}/{name}: expected shape {shape}, got {a.shape}")
+        parts.append(a.reshape(-1))
+    return np.ascontiguousarray(np.concatenate(parts))
+
+
 def param_count(codes_dim: int = 6) -> int:
     return int(sum(np.prod(sh) for _, _, sh in param_spec(codes_dim)))
 
@@ -179,12 +198,28 @@ def random_params(codes_dim: int = 6, seed: int = 0, z_scale: float = 1.5) -> Di
 
 
 def random_full_params(codes_dim: int = 6, seed: int = 0) -> Dict[str, Dict[str, np.ndarray]]:
-    """A whole Vq3D checkpoint's worth of random tensors (encoder as `random_params`, decoder
-    N(0, 0.02²)) — stands in for a real `params.npz`, which is not available offline."""
+    """A whole Vq3D checkpoint's worth of random tensors (stands in for a real `params.npz`,
+    which is not available offline). Encoder as `random_params`; decoder weights truncated
+    normal with σ = 1/sqrt(fan_in), biases / LN offsets N(0, 0.1²), LN scales 1 + N(0, 0.1²),
+    IPA point weights softplus⁻¹(1) + N(0, 0.1²) — activations stay O(1) through the decoder
+    and structure module, so decode parity tests exercise every path."""
     out = random_params(codes_dim, seed)
     rng = np.random.default_rng(seed + 1)
     for mod, name, shape in decoder_param_spec(codes_dim):
-        out.setdefault(mod, {})[name] = (0.02 * rng.standard_normal(shape)).astype(np.float32)
+        stacked = mod.startswith(US + "/cross_attn_scaler_iteration")
+        core = shape[1:] if stacked else shape
+        if name in ("w", "weights", "query_w", "key_w", "value_w", "gating_w", "output_w"):
+            fan_in = core[0] * core[1] if name == "output_w" else core[0]
+            v = np.clip(rng.standard_normal(shape), -2, 2) / np.sqrt(fan_in)
+        elif name == "scale":
+            v = 1.0 + 0.1 * rng.standard_normal(shape)
+        elif name in ("gating_b",):
+            v = 1.0 + 0.1 * rng.standard_normal(shape)
+        elif name == "trainable_point_weights":
+            v = np.log(np.e - 1.0) + 0.1 * rng.standard_normal(shape)
+        else:
+            v = 0.1 * rng.standard_normal(shape)
+        out.setdefault(mod, {})[name] = v.astype(np.float32)
     return out
 
 

@@ -265,6 +265,46 @@ class InferenceRunner:
         return TokenizeFn(cfg, devices, emit_aux)
 
     @staticmethod
+    def prepare_decode_fn(cfg: TokenizerConfig, devices: Sequence[int]) -> Callable:
+        return DecodeFn(cfg, devices)
+
+    @staticmethod
+    def prepare_token_to_code_fn(cfg: TokenizerConfig, devices: Sequence[int]) -> Callable:
+        return TokenToCodeFn(cfg)
+
+    @staticmethod
+    def decode_and_save_pdbs(random_key: Any, decode: Callable, indexes_to_codes_fn: Callable,
+                             sequences: List[str], model_params: ReplicatedParams, num_device: int,
+                             structure_save_path: str, batch_size_per_device: int, max_seq_len: int,
+                             downsampling_ratio: int, pad_token_id: int):
+        """(`inference_runner.py:326-437`): token files → `structures/structure_<stem>.pdb`,
+        same batching, masks, dummy-ALA residues and PDB format."""
+        from .structure_io import atom37_to_pdb
+        structure_dir = os.path.join(structure_save_path, "structures")
+        os.makedirs(structure_dir, exist_ok=False)
+        effective_batch_size = batch_size_per_device * num_device
+        num_iteration = len(sequences) // effective_batch_size + int((len(sequences) % effective_batch_size) > 0)
+        sequences = list(islice(cycle(sequences), num_iteration * effective_batch_size))
+        effective_length = max_seq_len // downsampling_ratio
+        for it in range(num_iteration):
+            start = it * effective_batch_size
+            files = sequences[start:start + effective_batch_size]
+            tokens_ids = load_and_build_batch(files, effective_length, pad_token_id)
+            tokens_mask = build_tokens_mask_from_sequence(tokens_ids, pad_token_id)
+            nodes_mask = build_nodes_mask_from_tokens_mask(tokens_mask, downsampling_ratio)
+            number_of_nodes = nodes_mask.sum(axis=-1)
+            out = decode(model_params, random_key,
+                         tokens_ids.reshape(num_device, batch_size_per_device, effective_length),
+                         tokens_mask.reshape(num_device, batch_size_per_device, effective_length))
+            pos = out["final_atom_positions"].reshape(effective_batch_size, -1, 37, 3)
+            mask = out["final_atom_mask"].reshape(effective_batch_size, -1, 37)
+            for k, f in enumerate(files):
+                n = int(number_of_nodes[k])
+                name = os.path.basename(f).split("_tokens.npy")[0]
+                with open(os.path.join(structure_dir, f"structure_{name}.pdb"), "w") as fh:
+                    fh.write(atom37_to_pdb(pos[k, :n], mask[k, :n], np.zeros(n, np.int64)))
+
+    @staticmethod
     def load_params(model_dir: str, local_devices: Sequence[int]) -> ReplicatedParams:
         """(`inference_runner.py:236-248`). Reads `model_dir/params.npz` only: the pickled
         treedef in `state_variables.npy` is never unpickled (the leaf order is
@@ -320,6 +360,93 @@ class InferenceRunner:
                     np.save(os.path.join(token_save_path, filename + "_tokens"), token_array)
                 if logger is not None:
                     logger.info(f"Took {time.perf_counter() - start_time}s to tokenize")
+
+
+# ------------------------------------------------------------------------------------- decode
+def build_tokens_mask_from_sequence(tokens_ids: np.ndarray, pad_token_id: int) -> np.ndarray:
+    """`inference_runner.py:86-95`: 1 before the first pad token, 0 from it on."""
+    tokens_ids = np.asarray(tokens_ids)
+    assert tokens_ids.ndim >= 2
+    is_eos = tokens_ids == pad_token_id
+    return np.where(np.cumsum(is_eos, axis=-1) == 0, 1, 0)
+
+
+def build_nodes_mask_from_tokens_mask(tokens_mask: np.ndarray, downsampling_ratio: int) -> np.ndarray:
+    """`inference_runner.py:98-111`."""
+    batch, seq_len = tokens_mask.shape
+    last_true_node = (downsampling_ratio * tokens_mask.sum(axis=-1)).reshape(batch, 1)
+    index = np.repeat(np.arange(downsampling_ratio * seq_len)[None], batch, axis=0)
+    return np.where(index < last_true_node, 1, 0)
+
+
+def load_and_build_batch(files_paths: Sequence[str], max_seq_len: int, pad_token_id: int) -> np.ndarray:
+    """`inference_runner.py:114-133`: token files → [B, max_seq_len] int32 padded with pad_token_id."""
+    def pad(seq, n):
+        return np.pad(seq, ((0, 0), (0, n - seq.shape[-1])), mode="constant", constant_values=pad_token_id)
+    return np.concatenate([pad(np.load(f, allow_pickle=False).astype(np.int32).reshape(1, -1)[:, :max_seq_len],
+                               max_seq_len) for f in files_paths])
+
+
+class TokenToCodeFn:
+    """`prepare_token_to_code_fn` (`inference_runner.py:224-233`): token ids → FSQ codes
+    (renorm off: digit − L//2), [..., D] float32. Exact integer arithmetic on the host."""
+
+    def __init__(self, cfg: TokenizerConfig):
+        self.levels = np.asarray(cfg.levels)
+
+    def __call__(self, model_params: Any, random_key: Any, tokens: np.ndarray) -> np.ndarray:
+        basis = np.concatenate(([1], np.cumprod(self.levels[:-1])))
+        t = np.asarray(tokens).astype(np.int64)[..., None]
+        return ((t // basis) % self.levels - self.levels // 2).astype(np.float32)
+
+
+class DecodeFn:
+    """`prepare_decode_fn` (`inference_runner.py:193-207`) for libpst: per-device decoder
+    contexts; `fn(model_params, random_key, tokens [n_dev, bpd, L], tokens_mask)` →
+    {"final_atom_positions" [n_dev, bpd, df·L, 37, 3], "final_atom_mask", "n_nodes"}.
+    Token ids (not codes) go to the GPU: indexes_to_codes runs inside the decoder."""
+
+    def __init__(self, cfg: TokenizerConfig, devices: Sequence[int]):
+        self.cfg = cfg
+        self.devices = list(devices)
+        self._ctx: Dict[Tuple[int, int], Any] = {}
+        self._pool = _cf.ThreadPoolExecutor(max_workers=max(1, len(self.devices)))
+
+    def _context(self, model_params: ReplicatedParams, dev: int):
+        key = (id(model_params), dev)
+        d = self._ctx.get(key)
+        if d is None:
+            blob = _params.pack_decoder(model_params.params, model_params.codes_dim)
+            d = _native.Decoder(dev, self.cfg.codebook_size, self.cfg.downsampling_ratio, blob, self.cfg.levels)
+            self._ctx[key] = d
+        return d
+
+    def __call__(self, model_params: ReplicatedParams, random_key: Any, tokens: np.ndarray,
+                 tokens_mask: np.ndarray) -> Dict[str, np.ndarray]:
+        tokens = np.asarray(tokens)
+        n_dev, bpd, L = tokens.shape
+        df = self.cfg.downsampling_ratio
+        n_tok = np.asarray(tokens_mask).reshape(n_dev, bpd, -1).sum(-1).astype(np.int64)
+
+        def run(i):
+            dec = self._context(model_params, self.devices[i])
+            return dec.decode([tokens[i, b, :n_tok[i, b]] for b in range(bpd)])
+
+        res = list(self._pool.map(run, range(n_dev)))
+        pos = np.zeros((n_dev, bpd, df * L, 37, 3), np.float32)
+        mask = np.zeros((n_dev, bpd, df * L, 37), np.float32)
+        for i in range(n_dev):
+            for b in range(bpd):
+                n = res[i][b].shape[0]
+                pos[i, b, :n] = res[i][b]
+                mask[i, b, :n, [0, 1, 2, 4]] = 1.0  # N, CA, C, O (model.py:547-556)
+        return {"final_atom_positions": pos, "final_atom_mask": mask, "n_nodes": df * n_tok}
+
+    def close(self):
+        for d in self._ctx.values():
+            d.close()
+        self._ctx.clear()
+        self._pool.shutdown(wait=True)
 
 
 def shard_for_rank(items: Sequence[Any], rank: int, world_size: int) -> List[Any]:

@@ -1,0 +1,56 @@
+"""Decode path on the GPU vs the reference model's own outputs (tests/golden/decode_golden_f64.npz:
+the reference decoder + structure module run in float64 under the shim, same random weights).
+The GPU computes in float32 with its own operation order, so every comparison has a tolerance;
+the tolerances are stated per quantity below."""
+import os
+
+import numpy as np
+import pytest
+import torch  # noqa: F401  (torch's HIP runtime first, see pst_amd._native)
+
+from pst_amd import params as P
+from pst_amd.config import LEVELS
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "decode_golden_f64.npz")
+
+# tolerances (float32 GPU vs float64 reference)
+TOL_SINGLE = 2e-5   # unit-norm single representation
+TOL_PAIR_REL = 2e-4  # pair representation, relative to its max |value|
+TOL_TRAJ = 2e-3     # quaternions (unit) and translations (Å) of all 8 layers
+TOL_ATOMS = 2e-3    # Å, final backbone coordinates
+
+
+def _cases():
+    if not os.path.exists(GOLD):
+        return []
+    F = np.load(GOLD)
+    return sorted({k.split("/")[0] for k in F.files})
+
+
+@pytest.mark.parametrize("case", _cases())
+def test_decode_matches_reference(case, monkeypatch):
+    monkeypatch.setenv("PST_DEBUG", "1")
+    from pst_amd._native import Decoder
+    F = np.load(GOLD)
+    cb, df, T, N, D, pseed = (int(v) for v in F[case + "/meta"])
+    blob = P.pack_decoder(P.random_full_params(D, pseed), D)
+    dec = Decoder(0, cb, df, blob)
+    atoms = dec.decode([F[case + "/tokens"]])[0]
+    single = dec.debug(0, N * 128).reshape(N, 128)
+    pair = dec.debug(1, N * N * 128).reshape(N, N, 128)
+    traj = dec.debug(2, 8 * N * 7).reshape(8, N, 7)
+    dec.close()
+    err = lambda a, b: float(np.max(np.abs(a - b)))
+    e_single = err(single, F[case + "/single"])
+    e_pair = err(pair, F[case + "/pair"]) / float(np.max(np.abs(F[case + "/pair"])))
+    e_traj = err(traj, F[case + "/traj"])
+    e_atoms = err(atoms, F[case + "/atom37"])
+    print(f"{case}: single {e_single:.2e} pair(rel) {e_pair:.2e} traj {e_traj:.2e} atoms {e_atoms:.2e}")
+    assert atoms.shape == (N, 37, 3)
+    assert e_single < TOL_SINGLE
+    assert e_pair < TOL_PAIR_REL
+    assert e_traj < TOL_TRAJ
+    assert e_atoms < TOL_ATOMS
+    mask = F[case + "/atom37_mask"].astype(bool)
+    assert np.all(atoms[~mask] == 0)
