@@ -54,3 +54,36 @@ def test_decode_matches_reference(case, monkeypatch):
     assert e_atoms < TOL_ATOMS
     mask = F[case + "/atom37_mask"].astype(bool)
     assert np.all(atoms[~mask] == 0)
+
+
+def test_decode_cli_end_to_end(tmp_path):
+    """tokens → `decode_tokens.py` → structures/structure_<stem>.pdb, coordinates equal to the
+    decoder's (PDB %8.3f rounding) and 4 backbone atoms per residue."""
+    import sys
+    from pst_amd._native import Decoder
+    from pst_amd.pdb import protein_structure_from_pdb_string
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "protein-structure-tokenizer_amd", "scripts"))
+    import decode_tokens
+    rng = np.random.default_rng(3)
+    tok_dir = tmp_path / "tokens"
+    tok_dir.mkdir()
+    toks = {"p1": rng.integers(0, 4096, 30), "p2": rng.integers(0, 4096, 57)}
+    for k, v in toks.items():
+        np.save(tok_dir / f"{k}_tokens.npy", v.astype(np.uint32).reshape(1, -1))
+    mdir = tmp_path / "model"
+    mdir.mkdir()
+    full = P.random_full_params(6, seed=9)
+    P.save_params_npz(str(mdir / "params.npz"), full)
+    out = tmp_path / "out"
+    decode_tokens.cli(["--tokens_dir", str(tok_dir), "--structure_save_path", str(out), "--weights_dir", str(mdir),
+                       "--batch_size_per_device", "2"])
+    dec = Decoder(0, 4096, 1, P.pack_decoder(full, 6))
+    for k, v in toks.items():
+        want = dec.decode([v])[0]
+        txt = (out / "structures" / f"structure_{k}.pdb").read_text()
+        s = protein_structure_from_pdb_string(txt)
+        assert s.nb_residues == len(v)
+        assert np.allclose(s.atom37_positions[:, [0, 1, 2, 4]], want[:, [0, 1, 2, 4]], atol=6e-4)
+        assert int(s.atom37_gt_exists.sum()) == 4 * len(v)
+    dec.close()
