@@ -15,10 +15,11 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "decode_golden_f64.npz")
 
 # tolerances (float32 GPU vs float64 reference)
-TOL_SINGLE = 2e-5   # unit-norm single representation
-TOL_PAIR_REL = 2e-4  # pair representation, relative to its max |value|
-TOL_TRAJ = 2e-3     # quaternions (unit) and translations (Å) of all 8 layers
-TOL_ATOMS = 2e-3    # Å, final backbone coordinates
+# (measured on MI355X, round 1: single 6e-7, pair 2e-6, traj 1.8e-4, atoms 1.8e-4 Å)
+TOL_SINGLE = 5e-6   # unit-norm single representation
+TOL_PAIR_REL = 2e-5  # pair representation, relative to its max |value|
+TOL_TRAJ = 1e-3     # quaternions (unit) and translations (Å) of all 8 layers
+TOL_ATOMS = 1e-3    # Å, final backbone coordinates
 
 
 def _cases():
