@@ -19,6 +19,8 @@
 #include <string>
 #include <vector>
 
+#include <rocblas/rocblas.h>
+
 #include "../../include/pst.h"
 #include "pst_backbone_tables.h"
 #include "pst_pe.h"
@@ -93,6 +95,20 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ X, int l
       *y = (flags & F_ACCUM) ? *y + v : v;
     }
   }
+}
+
+// epilogue of a library GEMM: y = act(y + b)
+__global__ void k_bias_act(float* __restrict__ Y, int ldy, const float* __restrict__ b, int64_t M, int N, int flags) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= M * N) return;
+  const int64_t r = e / N;
+  const int c = (int)(e - r * N);
+  float* y = Y + r * ldy + c;
+  float v = *y;
+  if (b) v = v + b[c];
+  if (flags & F_RELU_OUT) v = v > 0.0f ? v : 0.0f;
+  if (flags & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
+  *y = v;
 }
 
 // hk.LayerNorm over the last axis (C ≤ 512): mean, centred variance, eps 1e-5; one wave per row
@@ -513,6 +529,7 @@ struct pst_decoder {
   float* d_pe_tok = nullptr;   // PE(t; 512/df) [512/df][128]
   float* d_pe_rel = nullptr;   // PE(d; 512), d = -511..511 [1023][128]
   float* d_pw = nullptr;       // IPA point weights [12]
+  rocblas_handle blas = nullptr;  // the large pair-representation GEMMs (plain library GEMMs)
   DecWeights W{};
   // scratch (grow-only, sized for N = 512)
   void* ws = nullptr;
@@ -618,17 +635,52 @@ size_t walk_decoder(const float* base, int D, DecWeights* W) {
   return o;
 }
 
-// scaled-grid launcher helpers
-inline void gemm(hipStream_t st, const float* X, int ldx, const Lin& L, float* Y, int ldy, int M, int flags,
-                 const float* b_override = nullptr, bool use_bias = true) {
-  dim3 grid((L.out + 63) / 64, (M + 63) / 64);
-  hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, st, X, ldx, L.w, L.out, use_bias ? (b_override ? b_override : L.b) : nullptr,
-                     Y, ldy, M, L.out, L.in, flags);
+// GEMMs go to rocBLAS (row-major Y = X·W as column-major Yᵀ = Wᵀ·Xᵀ; accumulation via β = 1) with
+// a bias/activation epilogue; an input ReLU is applied into a scratch copy first. k_gemm is the
+// self-contained fallback (PST_DECODE_NO_BLAS=1). Set by decode_one for the current context.
+thread_local rocblas_handle t_blas = nullptr;
+thread_local float* t_relu_buf = nullptr;  // [512 × 2112] scratch for F_RELU_IN operands
+
+__global__ void k_relu_copy(const float* __restrict__ X, int ldx, float* __restrict__ Y, int64_t M, int K) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= M * K) return;
+  const int64_t r = e / K;
+  const int c = (int)(e - r * K);
+  const float v = X[r * ldx + c];
+  Y[e] = v > 0.0f ? v : 0.0f;
 }
-inline void gemm_raw(hipStream_t st, const float* X, int ldx, const float* Wt, int K, int N, const float* b, float* Y,
+
+inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, int K, int N, const float* b, float* Y,
                      int ldy, int M, int flags) {
+  if (t_blas && (!(flags & F_RELU_IN) || (int64_t)M * K <= 512 * 2112)) {
+    if (flags & F_RELU_IN) {
+      const int64_t n = (int64_t)M * K;
+      hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, ldx, t_relu_buf,
+                         (int64_t)M, K);
+      X = t_relu_buf;
+      ldx = K;
+    }
+    const float one = 1.0f, beta = (flags & F_ACCUM) ? 1.0f : 0.0f;
+    rocblas_sgemm(t_blas, rocblas_operation_none, rocblas_operation_none, N, M, K, &one, Wt, N, X, ldx, &beta, Y, ldy);
+    if (b || (flags & (F_RELU_OUT | F_SIGMOID_OUT))) {
+      const int64_t n = (int64_t)M * N;
+      hipLaunchKernelGGL(k_bias_act, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Y, ldy, b, (int64_t)M, N,
+                         flags & (F_RELU_OUT | F_SIGMOID_OUT));
+    }
+    return;
+  }
   dim3 grid((N + 63) / 64, (M + 63) / 64);
   hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, st, X, ldx, Wt, N, b, Y, ldy, M, N, K, flags);
+}
+
+inline void gemm(hipStream_t st, const float* X, int ldx, const Lin& L, float* Y, int ldy, int M, int flags,
+                 const float* b_override = nullptr, bool use_bias = true) {
+  gemm_any(st, X, ldx, L.w, L.in, L.out, use_bias ? (b_override ? b_override : L.b) : nullptr, Y, ldy, M, flags);
+}
+
+inline void gemm_raw(hipStream_t st, const float* X, int ldx, const float* Wt, int K, int N, const float* b, float* Y,
+                     int ldy, int M, int flags) {
+  gemm_any(st, X, ldx, Wt, K, N, b, Y, ldy, M, flags);
 }
 inline void layernorm(hipStream_t st, const float* X, int ldx, float* Y, int ldy, int M, int C, const LnP& p) {
   hipLaunchKernelGGL(k_layernorm, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, Y, ldy, M, C, p.s, p.o);
@@ -638,7 +690,7 @@ struct Scratch {
   float *orig_in, *orig, *res, *ln_a, *ln_b, *q, *k, *v, *gate, *wavg, *tr_h;
   float *left, *right, *P, *h1, *pair0, *catb, *lin_out, *lnz, *z, *zln, *b2d;
   float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
-  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14;
+  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf;
 };
 
 int ensure_ws(pst_decoder* dec, Scratch* S) {
@@ -658,7 +710,7 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
                 {&S->qpg, NN * 144},     {&S->kvpg, NN * 432},   {&S->feat, NN * 2112},  {&S->upd, NN * 6},
                 {&S->aff, NN * 7},       {&S->rot, NN * 9},      {&S->sca, NN * 128},    {&S->scb, NN * 128},
                 {&S->sct, NN * 128},     {&S->unnorm, NN * 6},   {&S->angles, 8 * NN * 6}, {&S->traj, 8 * NN * 7},
-                {&S->atom37, NN * 111},  {&S->atom14, NN * 42}};
+                {&S->atom37, NN * 111},  {&S->atom14, NN * 42},  {&S->relu_buf, NN * 2112}};
   size_t total = 0;
   for (auto& it : items) total += (it.n * sizeof(float) + 255) / 256 * 256;
   if (!dec->ws) {
@@ -680,6 +732,8 @@ int decode_one(pst_decoder* dec, Scratch& S, const uint32_t* d_tok, int T, bool 
   hipStream_t st = dec->stream;
   const int N = T * dec->df;
   if (T <= 0) return PST_OK;
+  t_blas = getenv("PST_DECODE_NO_BLAS") ? nullptr : dec->blas;
+  t_relu_buf = S.relu_buf;
   // ---- upsampler (CrossAttentionScaler, use_original_posenc)
   hipLaunchKernelGGL(k_up_init, dim3(T), dim3(128), 0, st, d_tok, T, dec->d_levels, dec->D, W.up_proj.w, W.up_proj.b,
                      dec->d_pe_tok, S.orig_in);
@@ -830,6 +884,9 @@ int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* 
   };
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&dec->stream, hipStreamNonBlocking) != hipSuccess)
     return bad("hip stream creation failed");
+  if (rocblas_create_handle(&dec->blas) != rocblas_status_success ||
+      rocblas_set_stream(dec->blas, dec->stream) != rocblas_status_success)
+    return bad("rocblas handle creation failed");
   if (hipMalloc(&dec->d_blob, n_params * sizeof(float)) != hipSuccess ||
       hipMemcpy(dec->d_blob, params, n_params * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
     return bad("decoder weight upload failed");
@@ -869,6 +926,7 @@ int pst_decoder_destroy(pst_decoder* dec) {
   for (void* p : {(void*)dec->d_blob, (void*)dec->d_levels, (void*)dec->d_pe_node, (void*)dec->d_pe_tok,
                   (void*)dec->d_pe_rel, (void*)dec->d_pw, dec->ws})
     if (p) (void)hipFree(p);
+  if (dec->blas) (void)rocblas_destroy_handle(dec->blas);
   if (dec->stream) (void)hipStreamDestroy(dec->stream);
   delete dec;
   return PST_OK;

@@ -1,0 +1,42 @@
+"""Decode-path throughput: B proteins × T tokens (random ids, random-init weights) through
+pst_decoder_decode (host token ids in, host atom37 out). Prints one JSON line.
+
+    python tools/bench_decode.py [--proteins 8] [--tokens 256] [--codebook 4096] [--df 1] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "protein-structure-tokenizer_amd"))
+import torch  # noqa: E402,F401  (torch's HIP runtime first)
+
+from pst_amd import params as P  # noqa: E402
+from pst_amd._native import Decoder  # noqa: E402
+from pst_amd.config import LEVELS  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--proteins", type=int, default=8)
+ap.add_argument("--tokens", type=int, default=256)
+ap.add_argument("--codebook", type=int, default=4096)
+ap.add_argument("--df", type=int, default=1)
+ap.add_argument("--reps", type=int, default=3)
+a = ap.parse_args()
+D = len(LEVELS[a.codebook])
+dec = Decoder(0, a.codebook, a.df, P.pack_decoder(P.random_full_params(D, 5), D))
+rng = np.random.default_rng(0)
+toks = [rng.integers(0, a.codebook, a.tokens) for _ in range(a.proteins)]
+dec.decode(toks[:1])
+t0 = time.perf_counter()
+for _ in range(a.reps):
+    out = dec.decode(toks)
+dt = (time.perf_counter() - t0) / a.reps
+N = a.tokens * a.df
+print(json.dumps({"path": "decode (tokens -> backbone atom37)", "proteins": a.proteins, "tokens_per_protein": a.tokens,
+                  "residues_per_protein": N, "codebook": a.codebook, "df": a.df, "ms_per_batch": round(dt * 1e3, 2),
+                  "residues_per_s": round(a.proteins * N / dt, 1), "finite": bool(all(np.isfinite(o).all() for o in out))}))
+dec.close()
