@@ -111,7 +111,8 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
 /*
  * Same on device buffers (d_* in HBM of ctx's device), asynchronous on ctx's stream.
  * prot_offsets stays a HOST array (it sizes the launch). Outputs are device buffers with the
- * layout of pst_tokenize. Call pst_sync before reading them.
+ * layout of pst_tokenize; d_n_nodes_out is required (the graph build writes it), d_n_tokens_out
+ * may be NULL. Call pst_sync before reading them.
  */
 int pst_tokenize_device(pst_ctx* ctx, const double* d_atom_pos, const uint8_t* d_atom_flags,
                         const int64_t* prot_offsets, int32_t n_prot, uint32_t* d_tokens_out,

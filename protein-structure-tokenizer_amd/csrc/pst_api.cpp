@@ -433,6 +433,7 @@ int validate(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot) {
   if (offsets[0] != 0) return fail(ctx, PST_E_INVALID, "prot_offsets[0] must be 0");
   for (int b = 0; b < n_prot; ++b) {
     int64_t r = offsets[b + 1] - offsets[b];
+    if (r < 0) return fail(ctx, PST_E_INVALID, "prot_offsets must be non-decreasing");
     if (r > ctx->desc.seq_max_size)
       return fail(ctx, PST_E_TOO_LARGE,
                   "We currently don't support protein with more than " + std::to_string(ctx->desc.seq_max_size) +
@@ -705,6 +706,8 @@ int pst_tokenize_device(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flag
                         int32_t n_prot, uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes) {
   if (!ctx) return PST_E_INVALID;
   ctx->err.clear();
+  if (!d_pos || !d_flags || !d_tokens || !d_nnodes)
+    return fail(ctx, PST_E_INVALID, "null device buffer (positions, flags, tokens and n_nodes are required)");
   int rc = validate(ctx, offsets, n_prot);
   if (rc) return rc;
   HIPCHK(hipSetDevice(ctx->device));
@@ -719,6 +722,7 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
                  int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
   if (!ctx) return PST_E_INVALID;
   ctx->err.clear();
+  if (!atom_pos || !atom_flags || !tokens_out) return fail(ctx, PST_E_INVALID, "null host buffer");
   int rc = validate(ctx, offsets, n_prot);
   if (rc) return rc;
   HIPCHK(hipSetDevice(ctx->device));

@@ -187,3 +187,23 @@ def test_tiny_and_empty_proteins(df):
     for b, s in enumerate(samples):
         o = O.tokenize(blob, LEVELS[cb], df, s.atom37_positions, s.atom_flags())
         assert np.array_equal(tok[off[b]: off[b] + nt[b]], o["tokens"])
+
+
+def test_invalid_inputs_rejected():
+    import ctypes
+    from pst_amd import _native
+    tk = tokenizer()
+    s = synthetic.synthetic_protein(60, 1)
+    pos, flags, off = _native.pack_samples([s, s])
+    with pytest.raises(ValueError, match="non-decreasing"):
+        tk.tokenize_packed(pos, flags, np.array([0, 60, 50], np.int64))
+    with pytest.raises(ValueError, match="prot_offsets\\[0\\]"):
+        tk.tokenize_packed(pos, flags, np.array([1, 61, 120], np.int64))
+    with pytest.raises(ValueError):
+        tk.tokenize_packed(pos, flags, np.array([0], np.int64))  # empty batch
+    L = _native.lib()
+    nt = np.zeros(2, np.int32)
+    rc = L.pst_tokenize(tk._h, None, _native._ptr(flags), _native._ptr(off), 2, None, _native._ptr(nt), None)
+    assert rc == _native.PST_E_INVALID
+    # the context still works after rejected calls
+    assert np.array_equal(tk.tokenize([s])[0], O.tokenize(P.random_blob(6, 1234), LEVELS[4096], 1, s.atom37_positions, s.atom_flags())["tokens"])
