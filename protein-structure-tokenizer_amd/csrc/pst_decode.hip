@@ -97,18 +97,19 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ X, int l
   }
 }
 
-// epilogue of a library GEMM: y = act(y + b)
-__global__ void k_bias_act(float* __restrict__ Y, int ldy, const float* __restrict__ b, int64_t M, int N, int flags) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= M * N) return;
-  const int64_t r = e / N;
-  const int c = (int)(e - r * N);
-  float* y = Y + r * ldy + c;
-  float v = *y;
-  if (b) v = v + b[c];
-  if (flags & F_RELU_OUT) v = v > 0.0f ? v : 0.0f;
-  if (flags & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
-  *y = v;
+// epilogue of a library GEMM: y = act(y + b); a wave per row, 4 rows per block
+__global__ __launch_bounds__(256) void k_bias_act(float* __restrict__ Y, int ldy, const float* __restrict__ b,
+                                                  int64_t M, int N, int flags) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= M) return;
+  float* y = Y + r * ldy;
+  for (int c = threadIdx.x & 63; c < N; c += 64) {
+    float v = y[c];
+    if (b) v = v + b[c];
+    if (flags & F_RELU_OUT) v = v > 0.0f ? v : 0.0f;
+    if (flags & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
+    y[c] = v;
+  }
 }
 
 // hk.LayerNorm over the last axis (C ≤ 512): mean, centred variance, eps 1e-5; one wave per row
@@ -160,12 +161,35 @@ __global__ void k_spherical(float* __restrict__ X, int M) {
   x[lane + 64] = b / d;
 }
 
+// A group of proteins decoded together: rows of every per-token / per-node / per-pair tensor are
+// the proteins' rows concatenated; per-protein kernels find their protein through these maps.
+struct DecBatch {
+  int32_t B;
+  const int64_t* tok_off;   // [B+1]
+  const int64_t* node_off;  // [B+1]
+  const int64_t* pair_off;  // [B+1] (N_b² rows per protein)
+  const int32_t* tok_prot;  // [T_total]
+  const int32_t* node_prot; // [N_total]
+};
+
+__device__ __forceinline__ int pair_protein(const DecBatch& bt, int64_t p) {
+  int lo = 0, hi = bt.B - 1;
+  while (lo < hi) {  // last b with pair_off[b] <= p
+    const int mid = (lo + hi + 1) >> 1;
+    if (bt.pair_off[mid] <= p) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 // codes (FSQ grid, renorm off: digit - L/2) → up_proj → [PE(t; T_pad) | up] rows of `orig_in`
-__global__ void k_up_init(const uint32_t* __restrict__ tokens, int T, const int* __restrict__ levels, int D,
-                          const float* __restrict__ w_up, const float* __restrict__ b_up,
-                          const float* __restrict__ pe_tok, float* __restrict__ orig_in) {
-  const int t = blockIdx.x, c = threadIdx.x;  // 128 threads
-  if (t >= T) return;
+__global__ void k_up_init(const uint32_t* __restrict__ tokens, DecBatch bt, int64_t T_total,
+                          const int* __restrict__ levels, int D, const float* __restrict__ w_up,
+                          const float* __restrict__ b_up, const float* __restrict__ pe_tok, float* __restrict__ orig_in) {
+  const int64_t t = blockIdx.x;
+  const int c = threadIdx.x;  // 128 threads
+  if (t >= T_total) return;
+  const int64_t tl = t - bt.tok_off[bt.tok_prot[t]];
   uint32_t tok = tokens[t];
   float code[8];
   uint32_t basis = 1;
@@ -177,26 +201,38 @@ __global__ void k_up_init(const uint32_t* __restrict__ tokens, int T, const int*
   }
   float acc = 0.0f;
   for (int d = 0; d < D; ++d) acc = __builtin_fmaf(code[d], w_up[d * 128 + c], acc);
-  orig_in[(int64_t)t * 256 + c] = pe_tok[(int64_t)t * 128 + c];
-  orig_in[(int64_t)t * 256 + 128 + c] = acc + b_up[c];
+  orig_in[t * 256 + c] = pe_tok[tl * 128 + c];
+  orig_in[t * 256 + 128 + c] = acc + b_up[c];
 }
 
-// Upsampler attention, gated (modules.py:271-382): one wave per (node i, head h); all T keys real
+// resampled track init: node i of its protein gets PE(i_local; 512)
+__global__ void k_node_pe(const float* __restrict__ pe_node, DecBatch bt, int64_t N_total, float* __restrict__ res) {
+  const int64_t i = blockIdx.x;
+  if (i >= N_total) return;
+  const int64_t il = i - bt.node_off[bt.node_prot[i]];
+  res[i * 128 + threadIdx.x] = pe_node[il * 128 + threadIdx.x];
+}
+
+// Upsampler attention, gated (modules.py:271-382): one wave per (node i, head h) over the T
+// tokens of i's protein (the only unmasked keys)
 __global__ __launch_bounds__(256) void k_up_attn(const float* __restrict__ q, const float* __restrict__ k,
                                                  const float* __restrict__ v, const float* __restrict__ gate,
-                                                 float* __restrict__ out, int N, int T) {
+                                                 float* __restrict__ out, DecBatch bt, int64_t N_total) {
   __shared__ float wsh[4][512];
   const int lane = threadIdx.x & 63, h = threadIdx.x >> 6;
-  const int i = blockIdx.x;
-  if (i >= N) return;
-  const float* qi = q + (int64_t)i * 128 + h * 32;
+  const int64_t i = blockIdx.x;
+  if (i >= N_total) return;
+  const int b = bt.node_prot[i];
+  const int64_t t0 = bt.tok_off[b];
+  const int T = (int)(bt.tok_off[b + 1] - t0);
+  const float* qi = q + i * 128 + h * 32;
   float l[8];
   float mx = -INFINITY;
   for (int s = 0; s < 8; ++s) {
     int j = lane + 64 * s;
     float acc = 0.0f;
     if (j < T) {
-      const float* kj = k + (int64_t)j * 128 + h * 32;
+      const float* kj = k + (t0 + j) * 128 + h * 32;
       for (int c = 0; c < 32; ++c) acc = __builtin_fmaf(qi[c], kj[c], acc);
     }
     l[s] = j < T ? acc : -INFINITY;
@@ -218,25 +254,32 @@ __global__ __launch_bounds__(256) void k_up_attn(const float* __restrict__ q, co
   __syncthreads();
   if (lane < 32) {
     float acc = 0.0f;
-    for (int j = 0; j < T; ++j) acc = __builtin_fmaf(wsh[h][j], v[(int64_t)j * 128 + h * 32 + lane], acc);
-    out[(int64_t)i * 128 + h * 32 + lane] = acc * gate[(int64_t)i * 128 + h * 32 + lane];
+    for (int j = 0; j < T; ++j) acc = __builtin_fmaf(wsh[h][j], v[(t0 + j) * 128 + h * 32 + lane], acc);
+    out[i * 128 + h * 32 + lane] = acc * gate[i * 128 + h * 32 + lane];
   }
 }
 
-// P[i*N+j][c] = left[i][c] * right[j][c] (256 channels, einsum "nd,kd->nkd")
+// P[pair (i, j) of protein b][c] = left[i][c] * right[j][c] (256 channels, einsum "nd,kd->nkd")
 __global__ void k_pair_product(const float* __restrict__ left, const float* __restrict__ right, float* __restrict__ P,
-                               int N) {
+                               DecBatch bt) {
   const int64_t pr = blockIdx.x;
-  const int i = (int)(pr / N), j = (int)(pr % N), c = threadIdx.x;
-  P[pr * 256 + c] = left[(int64_t)i * 256 + c] * right[(int64_t)j * 256 + c];
+  const int b = pair_protein(bt, pr);
+  const int64_t n0 = bt.node_off[b];
+  const int64_t Nb = bt.node_off[b + 1] - n0, loc = pr - bt.pair_off[b];
+  const int64_t i = n0 + loc / Nb, j = n0 + loc % Nb;
+  const int c = threadIdx.x;
+  P[pr * 256 + c] = left[i * 256 + c] * right[j * 256 + c];
 }
 
-// C[i*N+j] = [PE(j - i; 512) | pair0[i*N+j]] (sequence_decoder.py:69-99)
+// C[pair (i, j)] = [PE(j - i; 512) | pair0[pair]] (sequence_decoder.py:69-99)
 __global__ void k_pair_concat(const float* __restrict__ pe_rel /*[1023][128], row = d + 511*/,
-                              const float* __restrict__ pair0, float* __restrict__ C, int N) {
+                              const float* __restrict__ pair0, float* __restrict__ C, DecBatch bt) {
   const int64_t pr = blockIdx.x;
-  const int i = (int)(pr / N), j = (int)(pr % N), c = threadIdx.x;
-  C[pr * 256 + c] = pe_rel[(int64_t)(j - i + 511) * 128 + c];
+  const int b = pair_protein(bt, pr);
+  const int64_t Nb = bt.node_off[b + 1] - bt.node_off[b], loc = pr - bt.pair_off[b];
+  const int il = (int)(loc / Nb), jl = (int)(loc % Nb);
+  const int c = threadIdx.x;
+  C[pr * 256 + c] = pe_rel[(int64_t)(jl - il + 511) * 128 + c];
   C[pr * 256 + 128 + c] = pair0[pr * 128 + c];
 }
 
@@ -316,33 +359,43 @@ __global__ void k_ipa_points(const float* __restrict__ qpl /*[N][144]*/, const f
 // softmax, then the 2112 output features [scalar 192 | local points x,y,z 3×96 | norms 96 |
 // pair 1536]. One workgroup per i.
 __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /*[N][192]*/,
-                                                  const float* __restrict__ kvs /*[N][384]*/,
-                                                  const float* __restrict__ qpg, const float* __restrict__ kvpg,
-                                                  const float* __restrict__ b2d /*[N][N][12], × sqrt(1/3)*/,
-                                                  const float* __restrict__ zln /*[N][N][128]*/,
+                                                  const float* __restrict__ kvs_all /*[N][384]*/,
+                                                  const float* __restrict__ qpg, const float* __restrict__ kvpg_all,
+                                                  const float* __restrict__ b2d_all /*[pairs][12], × sqrt(1/3)*/,
+                                                  const float* __restrict__ zln_all /*[pairs][128]*/,
                                                   const float* __restrict__ pw /*[12]*/,
                                                   const float* __restrict__ aff, const float* __restrict__ rot,
-                                                  float* __restrict__ feat /*[N][2112]*/, int N) {
+                                                  float* __restrict__ feat /*[N][2112]*/, DecBatch bt) {
   __shared__ float att[12][512];
   __shared__ float res_pt[12 * 8 * 3];
-  const int i = blockIdx.x, tid = threadIdx.x;
+  const int64_t ig = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int bprot = bt.node_prot[ig];
+  const int64_t n0 = bt.node_off[bprot];
+  const int N = (int)(bt.node_off[bprot + 1] - n0);
+  const int il = (int)(ig - n0);
+  // protein-local views: rows j of kvs/kvpg, pair rows (il, j) of b2d/zln
+  const float* kvs = kvs_all + n0 * 384;
+  const float* kvpg = kvpg_all + n0 * 432;
+  const float* b2d = b2d_all + (bt.pair_off[bprot] + (int64_t)il * N) * 12;
+  const float* zln = zln_all + (bt.pair_off[bprot] + (int64_t)il * N) * 128;
   const float sw = 0.144337567297406f;  // sqrt(1 / (3 * 16))
   // logits
   for (int e = tid; e < 12 * N; e += 256) {
     const int h = e / N, j = e - h * N;
     float sc = 0.0f;
-    const float* q = qs + (int64_t)i * 192 + h * 16;
+    const float* q = qs + ig * 192 + h * 16;
     const float* k = kvs + (int64_t)j * 384 + h * 32;
     for (int c = 0; c < 16; ++c) sc = __builtin_fmaf(sw * q[c], k[c], sc);
     float pt = 0.0f;
     for (int p = 0; p < 4; ++p) {
-      const float* qp = qpg + (((int64_t)i * 12 + h) * 4 + p) * 3;
+      const float* qp = qpg + ((ig * 12 + h) * 4 + p) * 3;
       const float* kp = kvpg + (((int64_t)j * 12 + h) * 12 + p) * 3;
       const float dx = qp[0] - kp[0], dy = qp[1] - kp[1], dz = qp[2] - kp[2];
       const float d2 = (dx * dx + dy * dy) + dz * dz;
       pt += pw[h] * d2;
     }
-    att[h][j] = (sc + (-0.5f * pt)) + b2d[((int64_t)i * N + j) * 12 + h];
+    att[h][j] = (sc + (-0.5f * pt)) + b2d[(int64_t)j * 12 + h];
   }
   __syncthreads();
   // softmax per head (waves 0..3 take heads h, h+4, h+8)
@@ -363,7 +416,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
     }
   }
   __syncthreads();
-  float* f = feat + (int64_t)i * 2112;
+  float* f = feat + ig * 2112;
   // scalar values (192) and global value points (288)
   for (int o = tid; o < 192 + 288; o += 256) {
     float acc = 0.0f;
@@ -382,7 +435,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   {
     const int c = tid & 127, hg = tid >> 7;
     float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const float* zr = zln + (int64_t)i * N * 128 + c;
+    const float* zr = zln + c;
     for (int j = 0; j < N; ++j) {
       const float zv = zr[(int64_t)j * 128];
 #pragma unroll
@@ -395,8 +448,8 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   // global → local frame of i (invert_point) and norms
   if (tid < 96) {
     const int h = tid / 8, p = tid % 8;
-    const float* R = rot + i * 9;
-    const float* tr = aff + i * 7 + 4;
+    const float* R = rot + ig * 9;
+    const float* tr = aff + ig * 7 + 4;
     const float gx = res_pt[(h * 8 + p) * 3 + 0] - tr[0];
     const float gy = res_pt[(h * 8 + p) * 3 + 1] - tr[1];
     const float gz = res_pt[(h * 8 + p) * 3 + 2] - tr[2];
@@ -641,30 +694,28 @@ size_t walk_decoder(const float* base, int D, DecWeights* W) {
 thread_local rocblas_handle t_blas = nullptr;
 thread_local float* t_relu_buf = nullptr;  // [512 × 2112] scratch for F_RELU_IN operands
 
-__global__ void k_relu_copy(const float* __restrict__ X, int ldx, float* __restrict__ Y, int64_t M, int K) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= M * K) return;
-  const int64_t r = e / K;
-  const int c = (int)(e - r * K);
-  const float v = X[r * ldx + c];
-  Y[e] = v > 0.0f ? v : 0.0f;
+__global__ __launch_bounds__(256) void k_relu_copy(const float* __restrict__ X, int ldx, float* __restrict__ Y,
+                                                   int64_t M, int K) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= M) return;
+  for (int c = threadIdx.x & 63; c < K; c += 64) {
+    const float v = X[r * ldx + c];
+    Y[r * K + c] = v > 0.0f ? v : 0.0f;
+  }
 }
 
 inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, int K, int N, const float* b, float* Y,
                      int ldy, int M, int flags) {
   if (t_blas && (!(flags & F_RELU_IN) || (int64_t)M * K <= 512 * 2112)) {
     if (flags & F_RELU_IN) {
-      const int64_t n = (int64_t)M * K;
-      hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, ldx, t_relu_buf,
-                         (int64_t)M, K);
+      hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, X, ldx, t_relu_buf, (int64_t)M, K);
       X = t_relu_buf;
       ldx = K;
     }
     const float one = 1.0f, beta = (flags & F_ACCUM) ? 1.0f : 0.0f;
     rocblas_sgemm(t_blas, rocblas_operation_none, rocblas_operation_none, N, M, K, &one, Wt, N, X, ldx, &beta, Y, ldy);
     if (b || (flags & (F_RELU_OUT | F_SIGMOID_OUT))) {
-      const int64_t n = (int64_t)M * N;
-      hipLaunchKernelGGL(k_bias_act, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Y, ldy, b, (int64_t)M, N,
+      hipLaunchKernelGGL(k_bias_act, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, Y, ldy, b, (int64_t)M, N,
                          flags & (F_RELU_OUT | F_SIGMOID_OUT));
     }
     return;
@@ -686,33 +737,51 @@ inline void layernorm(hipStream_t st, const float* X, int ldx, float* Y, int ldy
   hipLaunchKernelGGL(k_layernorm, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, Y, ldy, M, C, p.s, p.o);
 }
 
+// group capacities: a group holds proteins while Σ N_b ≤ kNodeCap and Σ N_b² ≤ kPairCap
+// (one 512-residue protein is 2^18 pairs; the pair buffers are ≈ 5.7 KB per pair)
+constexpr int64_t kNodeCap = 8192;
+constexpr int64_t kPairCap = int64_t(1) << 20;
+
 struct Scratch {
   float *orig_in, *orig, *res, *ln_a, *ln_b, *q, *k, *v, *gate, *wavg, *tr_h;
   float *left, *right, *P, *h1, *pair0, *catb, *lin_out, *lnz, *z, *zln, *b2d;
   float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
   float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf;
+  int64_t *tok_off, *node_off, *pair_off;
+  int32_t *tok_prot, *node_prot;
+  uint32_t* tokens;
 };
 
 int ensure_ws(pst_decoder* dec, Scratch* S) {
-  const size_t NN = 512, NP = NN * NN;
+  const size_t NN = kNodeCap, NP = kPairCap;
   struct It {
-    float** p;
-    size_t n;
+    void** p;
+    size_t bytes;
   };
-  It items[] = {{&S->orig_in, NN * 256}, {&S->orig, NN * 128},   {&S->res, NN * 128},    {&S->ln_a, NN * 128},
-                {&S->ln_b, NN * 128},    {&S->q, NN * 128},      {&S->k, NN * 128},      {&S->v, NN * 128},
-                {&S->gate, NN * 128},    {&S->wavg, NN * 128},   {&S->tr_h, NN * 256},   {&S->left, NN * 256},
-                {&S->right, NN * 256},   {&S->P, NP * 256},      {&S->h1, NP * 256},     {&S->pair0, NP * 128},
-                {&S->catb, NP * 256},    {&S->lin_out, NP * 128}, {&S->lnz, NP * 128},   {&S->z, NP * 128},
-                {&S->zln, NP * 128},     {&S->b2d, NP * 12},     {&S->single_ln, NN * 128}, {&S->act, NN * 384},
-                {&S->init_act, NN * 128}, {&S->act_ln, NN * 384}, {&S->tmp384a, NN * 384}, {&S->tmp384b, NN * 384},
-                {&S->qs, NN * 192},      {&S->kvs, NN * 384},    {&S->qpl, NN * 144},    {&S->kvpl, NN * 432},
-                {&S->qpg, NN * 144},     {&S->kvpg, NN * 432},   {&S->feat, NN * 2112},  {&S->upd, NN * 6},
-                {&S->aff, NN * 7},       {&S->rot, NN * 9},      {&S->sca, NN * 128},    {&S->scb, NN * 128},
-                {&S->sct, NN * 128},     {&S->unnorm, NN * 6},   {&S->angles, 8 * NN * 6}, {&S->traj, 8 * NN * 7},
-                {&S->atom37, NN * 111},  {&S->atom14, NN * 42},  {&S->relu_buf, NN * 2112}};
+  const size_t F = sizeof(float);
+  It items[] = {{(void**)&S->orig_in, NN * 256 * F}, {(void**)&S->orig, NN * 128 * F}, {(void**)&S->res, NN * 128 * F},
+                {(void**)&S->ln_a, NN * 128 * F},    {(void**)&S->ln_b, NN * 128 * F}, {(void**)&S->q, NN * 128 * F},
+                {(void**)&S->k, NN * 128 * F},       {(void**)&S->v, NN * 128 * F},    {(void**)&S->gate, NN * 128 * F},
+                {(void**)&S->wavg, NN * 128 * F},    {(void**)&S->tr_h, NN * 256 * F}, {(void**)&S->left, NN * 256 * F},
+                {(void**)&S->right, NN * 256 * F},   {(void**)&S->P, NP * 256 * F},    {(void**)&S->h1, NP * 256 * F},
+                {(void**)&S->pair0, NP * 128 * F},   {(void**)&S->catb, NP * 256 * F}, {(void**)&S->lin_out, NP * 128 * F},
+                {(void**)&S->lnz, NP * 128 * F},     {(void**)&S->z, NP * 128 * F},    {(void**)&S->zln, NP * 128 * F},
+                {(void**)&S->b2d, NP * 12 * F},      {(void**)&S->single_ln, NN * 128 * F},
+                {(void**)&S->act, NN * 384 * F},     {(void**)&S->init_act, NN * 128 * F},
+                {(void**)&S->act_ln, NN * 384 * F},  {(void**)&S->tmp384a, NN * 384 * F},
+                {(void**)&S->tmp384b, NN * 384 * F}, {(void**)&S->qs, NN * 192 * F},   {(void**)&S->kvs, NN * 384 * F},
+                {(void**)&S->qpl, NN * 144 * F},     {(void**)&S->kvpl, NN * 432 * F}, {(void**)&S->qpg, NN * 144 * F},
+                {(void**)&S->kvpg, NN * 432 * F},    {(void**)&S->feat, NN * 2112 * F}, {(void**)&S->upd, NN * 6 * F},
+                {(void**)&S->aff, NN * 7 * F},       {(void**)&S->rot, NN * 9 * F},    {(void**)&S->sca, NN * 128 * F},
+                {(void**)&S->scb, NN * 128 * F},     {(void**)&S->sct, NN * 128 * F},  {(void**)&S->unnorm, NN * 6 * F},
+                {(void**)&S->angles, 8 * NN * 6 * F}, {(void**)&S->traj, 8 * NN * 7 * F},
+                {(void**)&S->atom37, NN * 111 * F},  {(void**)&S->atom14, NN * 42 * F},
+                {(void**)&S->relu_buf, NN * 2112 * F},
+                {(void**)&S->tok_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->node_off, (NN + 1) * sizeof(int64_t)},
+                {(void**)&S->pair_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->tok_prot, NN * sizeof(int32_t)},
+                {(void**)&S->node_prot, NN * sizeof(int32_t)}, {(void**)&S->tokens, NN * sizeof(uint32_t)}};
   size_t total = 0;
-  for (auto& it : items) total += (it.n * sizeof(float) + 255) / 256 * 256;
+  for (auto& it : items) total += (it.bytes + 255) / 256 * 256;
   if (!dec->ws) {
     hipError_t e = hipMalloc(&dec->ws, total);
     if (e != hipSuccess) return dfail(dec, PST_E_NOMEM, std::string("decoder workspace: ") + hipGetErrorString(e));
@@ -720,120 +789,144 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
   }
   char* p = (char*)dec->ws;
   for (auto& it : items) {
-    *it.p = (float*)p;
-    p += (it.n * sizeof(float) + 255) / 256 * 256;
+    *it.p = p;
+    p += (it.bytes + 255) / 256 * 256;
   }
   return PST_OK;
 }
 
-// decode one protein: tokens (device, T) → atom37 [N][37][3] (device), N = df·T
-int decode_one(pst_decoder* dec, Scratch& S, const uint32_t* d_tok, int T, bool keep_debug) {
+// Host view of one group: proteins [b0, b1) of the call.
+struct Group {
+  std::vector<int64_t> tok_off, node_off, pair_off;
+  std::vector<int32_t> tok_prot, node_prot;
+  std::vector<uint32_t> tokens;
+  int64_t T = 0, N = 0, NP = 0;
+  int B = 0;
+};
+
+// decode a group; atom37 of its nodes are left in S.atom37 (group order)
+int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) {
   const DecWeights& W = dec->W;
   hipStream_t st = dec->stream;
-  const int N = T * dec->df;
-  if (T <= 0) return PST_OK;
+  const int64_t T = G.T, N = G.N, NP = G.NP;
   t_blas = getenv("PST_DECODE_NO_BLAS") ? nullptr : dec->blas;
   t_relu_buf = S.relu_buf;
+  DCHK(hipMemcpyAsync(S.tokens, G.tokens.data(), sizeof(uint32_t) * T, hipMemcpyHostToDevice, st));
+  DCHK(hipMemcpyAsync(S.tok_off, G.tok_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
+  DCHK(hipMemcpyAsync(S.node_off, G.node_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
+  DCHK(hipMemcpyAsync(S.pair_off, G.pair_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
+  DCHK(hipMemcpyAsync(S.tok_prot, G.tok_prot.data(), sizeof(int32_t) * T, hipMemcpyHostToDevice, st));
+  DCHK(hipMemcpyAsync(S.node_prot, G.node_prot.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  DecBatch bt{G.B, S.tok_off, S.node_off, S.pair_off, S.tok_prot, S.node_prot};
+  const int Ni = (int)N;
   // ---- upsampler (CrossAttentionScaler, use_original_posenc)
-  hipLaunchKernelGGL(k_up_init, dim3(T), dim3(128), 0, st, d_tok, T, dec->d_levels, dec->D, W.up_proj.w, W.up_proj.b,
-                     dec->d_pe_tok, S.orig_in);
-  gemm(st, S.orig_in, 256, W.proj_original, S.orig, 128, T, 0);
-  DCHK(hipMemcpyAsync(S.res, dec->d_pe_node, sizeof(float) * N * 128, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(k_up_init, dim3((unsigned)T), dim3(128), 0, st, S.tokens, bt, T, dec->d_levels, dec->D,
+                     W.up_proj.w, W.up_proj.b, dec->d_pe_tok, S.orig_in);
+  gemm(st, S.orig_in, 256, W.proj_original, S.orig, 128, (int)T, 0);
+  hipLaunchKernelGGL(k_node_pe, dim3((unsigned)N), dim3(128), 0, st, dec->d_pe_node, bt, N, S.res);
   for (int b = 0; b < 3; ++b) {
-    layernorm(st, S.res, 128, S.ln_a, 128, N, 128, W.qn[b]);
-    layernorm(st, S.orig, 128, S.ln_b, 128, T, 128, W.dn[b]);
-    gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, N, 0);
-    gemm_raw(st, S.ln_a, 128, W.wg[b], 128, 128, W.gb[b], S.gate, 128, N, F_SIGMOID_OUT);
-    gemm_raw(st, S.ln_b, 128, W.wk[b], 128, 128, nullptr, S.k, 128, T, 0);
-    gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, T, 0);
-    // q · key_dim^-0.5 folded into the attention kernel's operand: scale q in place
-    hipLaunchKernelGGL(k_scale, dim3((N * 128 + 255) / 256), dim3(256), 0, st, S.q, N * 128, 0.176776695296637f);
-    hipLaunchKernelGGL(k_up_attn, dim3(N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, N, T);
-    gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, N, F_ACCUM);
-    // resampled transition (residual)
-    layernorm(st, S.res, 128, S.ln_a, 128, N, 128, W.rt_ln[b]);
-    gemm(st, S.ln_a, 128, W.rt1[b], S.tr_h, 256, N, F_RELU_OUT);
-    gemm(st, S.tr_h, 256, W.rt2[b], S.res, 128, N, F_ACCUM);
-    // original transition (residual)
-    layernorm(st, S.orig, 128, S.ln_b, 128, T, 128, W.ot_ln[b]);
-    gemm(st, S.ln_b, 128, W.ot1[b], S.tr_h, 256, T, F_RELU_OUT);
-    gemm(st, S.tr_h, 256, W.ot2[b], S.orig, 128, T, F_ACCUM);
+    layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.qn[b]);
+    layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.dn[b]);
+    gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, Ni, 0);
+    gemm_raw(st, S.ln_a, 128, W.wg[b], 128, 128, W.gb[b], S.gate, 128, Ni, F_SIGMOID_OUT);
+    gemm_raw(st, S.ln_b, 128, W.wk[b], 128, 128, nullptr, S.k, 128, (int)T, 0);
+    gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, (int)T, 0);
+    // q · key_dim^-0.5 (modules.py:346)
+    hipLaunchKernelGGL(k_scale, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.q, N * 128,
+                       0.176776695296637f);
+    hipLaunchKernelGGL(k_up_attn, dim3((unsigned)N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, bt, N);
+    gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, Ni, F_ACCUM);
+    layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.rt_ln[b]);
+    gemm(st, S.ln_a, 128, W.rt1[b], S.tr_h, 256, Ni, F_RELU_OUT);
+    gemm(st, S.tr_h, 256, W.rt2[b], S.res, 128, Ni, F_ACCUM);
+    layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.ot_ln[b]);
+    gemm(st, S.ln_b, 128, W.ot1[b], S.tr_h, 256, (int)T, F_RELU_OUT);
+    gemm(st, S.tr_h, 256, W.ot2[b], S.orig, 128, (int)T, F_ACCUM);
   }
-  hipLaunchKernelGGL(k_spherical, dim3((N + 3) / 4), dim3(256), 0, st, S.res, N);  // s_i
-  // ---- sequence decoder: pair representation
-  const int NP = N * N;
-  layernorm(st, S.res, 128, S.ln_a, 128, N, 128, W.pr_ln_in);
-  gemm(st, S.ln_a, 128, W.left, S.left, 256, N, 0);
-  gemm(st, S.ln_a, 128, W.right, S.right, 256, N, 0);
-  hipLaunchKernelGGL(k_pair_product, dim3(NP), dim3(256), 0, st, S.left, S.right, S.P, N);
-  gemm(st, S.P, 256, W.out1, S.h1, 256, NP, F_RELU_OUT);
-  gemm(st, S.h1, 256, W.out2, S.pair0, 128, NP, 0);
-  gemm(st, S.P, 256, W.right1, S.lin_out, 128, NP, 0);
-  hipLaunchKernelGGL(k_add, dim3((NP * 128 + 255) / 256), dim3(256), 0, st, S.pair0, S.lin_out, (int64_t)NP * 128);
-  layernorm(st, S.pair0, 128, S.pair0, 128, NP, 128, W.pr_ln_out);
-  hipLaunchKernelGGL(k_pair_concat, dim3(NP), dim3(128), 0, st, dec->d_pe_rel, S.pair0, S.catb, N);
-  gemm(st, S.catb, 256, W.seq_linear, S.lin_out, 128, NP, 0);
-  layernorm(st, S.lin_out, 128, S.lnz, 128, NP, 128, W.pt_ln);
-  gemm(st, S.lnz, 128, W.pt1, S.h1, 256, NP, F_RELU_OUT);
-  gemm(st, S.h1, 256, W.pt2, S.z, 128, NP, 0);  // z_ij (Transition output, no residual)
+  hipLaunchKernelGGL(k_spherical, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.res, Ni);  // s_i
+  // ---- sequence decoder: pair representation over each protein's N_b² pairs
+  const int NPi = (int)NP;
+  layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.pr_ln_in);
+  gemm(st, S.ln_a, 128, W.left, S.left, 256, Ni, 0);
+  gemm(st, S.ln_a, 128, W.right, S.right, 256, Ni, 0);
+  hipLaunchKernelGGL(k_pair_product, dim3((unsigned)NP), dim3(256), 0, st, S.left, S.right, S.P, bt);
+  gemm(st, S.P, 256, W.out1, S.h1, 256, NPi, F_RELU_OUT);
+  gemm(st, S.h1, 256, W.out2, S.pair0, 128, NPi, 0);
+  gemm(st, S.P, 256, W.right1, S.lin_out, 128, NPi, 0);
+  hipLaunchKernelGGL(k_add, dim3((unsigned)((NP * 128 + 255) / 256)), dim3(256), 0, st, S.pair0, S.lin_out, NP * 128);
+  layernorm(st, S.pair0, 128, S.pair0, 128, NPi, 128, W.pr_ln_out);
+  hipLaunchKernelGGL(k_pair_concat, dim3((unsigned)NP), dim3(128), 0, st, dec->d_pe_rel, S.pair0, S.catb, bt);
+  gemm(st, S.catb, 256, W.seq_linear, S.lin_out, 128, NPi, 0);
+  layernorm(st, S.lin_out, 128, S.lnz, 128, NPi, 128, W.pt_ln);
+  gemm(st, S.lnz, 128, W.pt1, S.h1, 256, NPi, F_RELU_OUT);
+  gemm(st, S.h1, 256, W.pt2, S.z, 128, NPi, 0);  // z_ij (Transition output, no residual)
   // ---- structure module
-  layernorm(st, S.res, 128, S.init_act, 128, N, 128, W.single_ln);
-  gemm(st, S.init_act, 128, W.init_proj, S.act, 384, N, 0);
-  layernorm(st, S.z, 128, S.zln, 128, NP, 128, W.pair_ln);
-  gemm(st, S.zln, 128, W.att2d, S.b2d, 12, NP, 0);
-  hipLaunchKernelGGL(k_scale, dim3((NP * 12 + 255) / 256), dim3(256), 0, st, S.b2d, NP * 12, 0.577350269189626f);
-  hipLaunchKernelGGL(k_affine_init, dim3((N + 63) / 64), dim3(64), 0, st, S.aff, S.rot, N);
+  layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
+  gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
+  layernorm(st, S.z, 128, S.zln, 128, NPi, 128, W.pair_ln);
+  gemm(st, S.zln, 128, W.att2d, S.b2d, 12, NPi, 0);
+  hipLaunchKernelGGL(k_scale, dim3((unsigned)((NP * 12 + 255) / 256)), dim3(256), 0, st, S.b2d, NP * 12,
+                     0.577350269189626f);
+  hipLaunchKernelGGL(k_affine_init, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, Ni);
   for (int it = 0; it < 8; ++it) {
-    gemm(st, S.act, 384, W.q_scalar, S.qs, 192, N, 0);
-    gemm(st, S.act, 384, W.kv_scalar, S.kvs, 384, N, 0);
-    gemm(st, S.act, 384, W.q_point, S.qpl, 144, N, 0);
-    gemm(st, S.act, 384, W.kv_point, S.kvpl, 432, N, 0);
-    hipLaunchKernelGGL(k_ipa_points, dim3(N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg, N);
-    hipLaunchKernelGGL(k_ipa_attn, dim3(N), dim3(256), 0, st, S.qs, S.kvs, S.qpg, S.kvpg, S.b2d, S.zln, dec->d_pw,
-                       S.aff, S.rot, S.feat, N);
-    gemm(st, S.feat, 2112, W.out_proj, S.act, 384, N, F_ACCUM);  // act += IPA
-    layernorm(st, S.act, 384, S.act, 384, N, 384, W.att_ln);
-    gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, N, F_RELU_OUT);
-    gemm(st, S.tmp384a, 384, W.tr[1], S.tmp384b, 384, N, F_RELU_OUT);
-    gemm(st, S.tmp384b, 384, W.tr[2], S.act, 384, N, F_ACCUM);  // += input_act
-    layernorm(st, S.act, 384, S.act, 384, N, 384, W.tr_ln);
-    gemm(st, S.act, 384, W.affine_update, S.upd, 6, N, 0);
-    hipLaunchKernelGGL(k_affine_update, dim3((N + 63) / 64), dim3(64), 0, st, S.aff, S.rot, S.upd, N);
+    gemm(st, S.act, 384, W.q_scalar, S.qs, 192, Ni, 0);
+    gemm(st, S.act, 384, W.kv_scalar, S.kvs, 384, Ni, 0);
+    gemm(st, S.act, 384, W.q_point, S.qpl, 144, Ni, 0);
+    gemm(st, S.act, 384, W.kv_point, S.kvpl, 432, Ni, 0);
+    hipLaunchKernelGGL(k_ipa_points, dim3((unsigned)N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg,
+                       Ni);
+    hipLaunchKernelGGL(k_ipa_attn, dim3((unsigned)N), dim3(256), 0, st, S.qs, S.kvs, S.qpg, S.kvpg, S.b2d, S.zln,
+                       dec->d_pw, S.aff, S.rot, S.feat, bt);
+    gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
+    layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
+    gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
+    gemm(st, S.tmp384a, 384, W.tr[1], S.tmp384b, 384, Ni, F_RELU_OUT);
+    gemm(st, S.tmp384b, 384, W.tr[2], S.act, 384, Ni, F_ACCUM);  // += input_act
+    layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.tr_ln);
+    gemm(st, S.act, 384, W.affine_update, S.upd, 6, Ni, 0);
+    hipLaunchKernelGGL(k_affine_update, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.upd, Ni);
     // MultiRigidSidechain: (0 + Lin(relu(act))) + Lin(relu(initial_act)), 2 residual blocks, angles
-    hipLaunchKernelGGL(k_zero, dim3((N * 128 + 255) / 256), dim3(256), 0, st, S.sca, N * 128);
-    gemm(st, S.act, 384, W.sc_in, S.sca, 128, N, F_RELU_IN | F_ACCUM);
-    gemm(st, S.init_act, 128, W.sc_in1, S.sca, 128, N, F_RELU_IN | F_ACCUM);
-    gemm(st, S.sca, 128, W.rb1, S.scb, 128, N, F_RELU_IN);
-    gemm(st, S.scb, 128, W.rb2, S.sca, 128, N, F_RELU_IN | F_ACCUM);
-    gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, N, F_RELU_IN);
-    gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, N, F_RELU_IN | F_ACCUM);
-    gemm(st, S.sca, 128, W.angles, S.unnorm, 6, N, F_RELU_IN);
+    hipLaunchKernelGGL(k_zero, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.sca, N * 128);
+    gemm(st, S.act, 384, W.sc_in, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
+    gemm(st, S.init_act, 128, W.sc_in1, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
+    gemm(st, S.sca, 128, W.rb1, S.scb, 128, Ni, F_RELU_IN);
+    gemm(st, S.scb, 128, W.rb2, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
+    gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, Ni, F_RELU_IN);
+    gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
+    gemm(st, S.sca, 128, W.angles, S.unnorm, 6, Ni, F_RELU_IN);
     const bool last = it == 7;
-    hipLaunchKernelGGL(k_sc_geom, dim3((N + 63) / 64), dim3(64), 0, st, S.aff, S.rot, S.unnorm, S.angles + it * 512 * 6,
-                       S.traj + it * 512 * 7, last ? S.atom37 : nullptr, last ? S.atom14 : nullptr, N);
+    hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.unnorm,
+                       S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7, last ? S.atom37 : nullptr,
+                       last ? S.atom14 : nullptr, Ni);
   }
   DCHK(hipGetLastError());
   if (keep_debug) {
-    const size_t o1 = dec->last_single.size();
-    dec->last_single.resize(o1 + (size_t)N * 128);
-    DCHK(hipMemcpyAsync(dec->last_single.data() + o1, S.res, sizeof(float) * N * 128, hipMemcpyDeviceToHost, st));
-    const size_t o2 = dec->last_pair.size();
-    dec->last_pair.resize(o2 + (size_t)NP * 128);
-    DCHK(hipMemcpyAsync(dec->last_pair.data() + o2, S.z, sizeof(float) * NP * 128, hipMemcpyDeviceToHost, st));
-    const size_t o3 = dec->last_traj.size();
-    dec->last_traj.resize(o3 + (size_t)8 * N * 7);
-    for (int it = 0; it < 8; ++it)
-      DCHK(hipMemcpyAsync(dec->last_traj.data() + o3 + (size_t)it * N * 7, S.traj + it * 512 * 7, sizeof(float) * N * 7,
-                          hipMemcpyDeviceToHost, st));
-    const size_t o4 = dec->last_angles.size();
-    dec->last_angles.resize(o4 + (size_t)8 * N * 6);
-    for (int it = 0; it < 8; ++it)
-      DCHK(hipMemcpyAsync(dec->last_angles.data() + o4 + (size_t)it * N * 6, S.angles + it * 512 * 6,
-                          sizeof(float) * N * 6, hipMemcpyDeviceToHost, st));
-    const size_t o5 = dec->last_atom14.size();
-    dec->last_atom14.resize(o5 + (size_t)N * 42);
-    DCHK(hipMemcpyAsync(dec->last_atom14.data() + o5, S.atom14, sizeof(float) * N * 42, hipMemcpyDeviceToHost, st));
+    std::vector<float> h((size_t)NP * 128 > (size_t)8 * N * 7 ? (size_t)NP * 128 : (size_t)8 * N * 7);
+    auto grab = [&](const float* src, size_t n) -> int {
+      DCHK(hipMemcpyAsync(h.data(), src, n * sizeof(float), hipMemcpyDeviceToHost, st));
+      DCHK(hipStreamSynchronize(st));
+      return PST_OK;
+    };
+    if (grab(S.res, (size_t)N * 128)) return PST_E_HIP;
+    dec->last_single.insert(dec->last_single.end(), h.begin(), h.begin() + N * 128);
+    if (grab(S.z, (size_t)NP * 128)) return PST_E_HIP;
+    dec->last_pair.insert(dec->last_pair.end(), h.begin(), h.begin() + NP * 128);
+    if (grab(S.atom14, (size_t)N * 42)) return PST_E_HIP;
+    dec->last_atom14.insert(dec->last_atom14.end(), h.begin(), h.begin() + N * 42);
+    // per-protein [8][N_b][...] blocks from the [8][kNodeCap][...] device layout
+    std::vector<float> tr((size_t)8 * kNodeCap * 7), an((size_t)8 * kNodeCap * 6);
+    DCHK(hipMemcpyAsync(tr.data(), S.traj, tr.size() * sizeof(float), hipMemcpyDeviceToHost, st));
+    DCHK(hipMemcpyAsync(an.data(), S.angles, an.size() * sizeof(float), hipMemcpyDeviceToHost, st));
     DCHK(hipStreamSynchronize(st));
+    for (int b = 0; b < G.B; ++b) {
+      const int64_t n0 = G.node_off[b], nb = G.node_off[b + 1] - n0;
+      for (int it = 0; it < 8; ++it) {
+        const float* t7 = tr.data() + ((size_t)it * kNodeCap + n0) * 7;
+        dec->last_traj.insert(dec->last_traj.end(), t7, t7 + nb * 7);
+        const float* a6 = an.data() + ((size_t)it * kNodeCap + n0) * 6;
+        dec->last_angles.insert(dec->last_angles.end(), a6, a6 + nb * 6);
+      }
+    }
   }
   return PST_OK;
 }
@@ -942,6 +1035,7 @@ int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* 
   const int64_t max_tok = 512 / dec->df;
   int64_t K = 1;
   for (int d = 0; d < dec->D; ++d) K *= dec->desc.levels[d];
+  if (token_offsets[0] != 0) return dfail(dec, PST_E_INVALID, "token_offsets[0] must be 0");
   for (int b = 0; b < n_prot; ++b) {
     const int64_t T = token_offsets[b + 1] - token_offsets[b];
     if (T < 0 || T > max_tok)
@@ -960,30 +1054,41 @@ int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* 
   dec->last_traj.clear();
   dec->last_angles.clear();
   dec->last_atom14.clear();
-  uint32_t* d_tok = nullptr;
-  DCHK(hipMalloc(&d_tok, sizeof(uint32_t) * 512));
-  int64_t node_off = 0;
-  for (int b = 0; b < n_prot; ++b) {
-    const int T = (int)(token_offsets[b + 1] - token_offsets[b]);
-    const int N = T * dec->df;
-    if (T > 0) {
-      hipError_t e = hipMemcpyAsync(d_tok, tokens + token_offsets[b], sizeof(uint32_t) * T, hipMemcpyHostToDevice,
-                                    dec->stream);
-      if (e == hipSuccess) rc = decode_one(dec, S, d_tok, T, keep);
-      else rc = dfail(dec, PST_E_HIP, hipGetErrorString(e));
-      if (rc == PST_OK) {
-        e = hipMemcpyAsync(atom37_out + node_off * 111, S.atom37, sizeof(float) * N * 111, hipMemcpyDeviceToHost,
-                           dec->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(dec->stream);
-        if (e != hipSuccess) rc = dfail(dec, PST_E_HIP, hipGetErrorString(e));
+  int64_t out_node = 0;
+  int b = 0;
+  while (b < n_prot) {
+    Group G;
+    G.tok_off.push_back(0);
+    G.node_off.push_back(0);
+    G.pair_off.push_back(0);
+    const int64_t out0 = out_node;
+    while (b < n_prot) {
+      const int64_t T = token_offsets[b + 1] - token_offsets[b], N = T * dec->df;
+      if (G.B > 0 && (G.N + N > kNodeCap || G.NP + N * N > kPairCap)) break;
+      if (n_nodes_out) n_nodes_out[b] = (int32_t)N;
+      if (T > 0) {  // empty proteins take no rows
+        G.tokens.insert(G.tokens.end(), tokens + token_offsets[b], tokens + token_offsets[b + 1]);
+        G.tok_prot.insert(G.tok_prot.end(), (size_t)T, G.B);
+        G.node_prot.insert(G.node_prot.end(), (size_t)N, G.B);
+        G.T += T;
+        G.N += N;
+        G.NP += N * N;
+        G.tok_off.push_back(G.T);
+        G.node_off.push_back(G.N);
+        G.pair_off.push_back(G.NP);
+        ++G.B;
       }
-      if (rc) break;
+      out_node += N;
+      ++b;
     }
-    if (n_nodes_out) n_nodes_out[b] = N;
-    node_off += N;
+    if (G.B == 0) continue;
+    rc = decode_group(dec, S, G, keep);
+    if (rc) return rc;
+    DCHK(hipMemcpyAsync(atom37_out + out0 * 111, S.atom37, sizeof(float) * G.N * 111, hipMemcpyDeviceToHost,
+                        dec->stream));
+    DCHK(hipStreamSynchronize(dec->stream));
   }
-  (void)hipFree(d_tok);
-  return rc;
+  return PST_OK;
 }
 
 int pst_decoder_debug(pst_decoder* dec, int32_t which, float* out, size_t n_floats) {

@@ -88,3 +88,22 @@ def test_decode_cli_end_to_end(tmp_path):
         assert np.allclose(s.atom37_positions[:, [0, 1, 2, 4]], want[:, [0, 1, 2, 4]], atol=6e-4)
         assert int(s.atom37_gt_exists.sum()) == 4 * len(v)
     dec.close()
+
+
+def test_grouped_decode_matches_single():
+    """Several proteins decoded in one call (grouped rows, one launch sequence per group) equal
+    the same proteins decoded one by one, within float32 reordering noise; empty token lists
+    give zero residues."""
+    from pst_amd._native import Decoder
+    rng = np.random.default_rng(11)
+    lens = [30, 0, 57, 128, 1]
+    toks = [rng.integers(0, 64000, n) for n in lens]
+    dec = Decoder(0, 64000, 2, P.pack_decoder(P.random_full_params(6, 4), 6))
+    together = dec.decode(toks)
+    assert [t.shape[0] for t in together] == [2 * n for n in lens]
+    for t, want_tok in zip(together, toks):
+        if len(want_tok) == 0:
+            continue
+        alone = dec.decode([want_tok])[0]
+        assert np.max(np.abs(t - alone)) < 1e-3
+    dec.close()
