@@ -171,7 +171,7 @@ __device__ int rank_select(const double* cen, int64_t base, int n, int rr, int c
   return rr;
 }
 
-#ifndef PST_KNN_SHFL
+#ifdef PST_KNN_ROUNDS
 // one DPP step of a lexicographic (distance, index) argmin: combine with the lane `ctrl` selects
 // (lanes the row mask excludes keep their own pair)
 __device__ __forceinline__ void argmin_dpp_step(double& d, int& s, int ctrl, int row_mask) {
@@ -219,6 +219,17 @@ __device__ __forceinline__ void wave_argmin(double& d, int& s) {
 }
 #endif
 
+// LDS of k_knn's radix select, one slice per wave
+__shared__ unsigned knn_hist[4][256];
+__shared__ double knn_sd[4][64];
+__shared__ int knn_ss[4][64];
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -247,9 +258,115 @@ __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
   }
   const int keep = n <= KNN ? n : KNN + 1;
   const int drop = n <= KNN ? 0 : 1;  // column 0 (self) dropped when n > k (protein_utils.py:700)
-  unsigned taken = 0;
   int my_s = -1;
   double my_d = 0.0;
+#ifndef PST_KNN_ROUNDS
+  {
+    // Radix select of the keep smallest (distance, index) pairs: 8 passes of an 8-bit histogram
+    // over the distance bits (non-negative doubles order like their bit patterns) find the exact
+    // keep-th distance T; ties at T are taken in index order; the selected pairs are ranked by
+    // counting (keep <= 51 entries) — the same order as the lexicographic argsort.
+    const int w = threadIdx.x >> 6;
+    unsigned* hist = knn_hist[w];
+    unsigned long long key[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) key[i] = (unsigned long long)__double_as_longlong(d[i]);
+    unsigned long long prefix = 0, mask = 0, lt_bound = 0;
+    int rem = keep;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hist[lane * 4 + q] = 0u;
+      wave_lds_sync();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int si = lane + 64 * i;
+        if (si < n && (key[i] & mask) == prefix) atomicAdd(&hist[(unsigned)(key[i] >> shift) & 255u], 1u);
+      }
+      wave_lds_sync();
+      unsigned c[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c[q] = hist[lane * 4 + q];
+      const unsigned tot = c[0] + c[1] + c[2] + c[3];
+      unsigned incl = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+      }
+      unsigned run = incl - tot;  // buckets before this lane's four
+      int found = -1;
+      unsigned below = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (found < 0 && run < (unsigned)rem && (unsigned)rem <= run + c[q]) {
+          found = lane * 4 + q;
+          below = run;
+        }
+        run += c[q];
+      }
+      const unsigned long long hit = __ballot(found >= 0);
+      const int wl = __builtin_ctzll(hit);
+      const unsigned cnt = (unsigned)__builtin_amdgcn_readlane((int)hist[found < 0 ? 0 : found], wl);
+      found = __builtin_amdgcn_readlane(found, wl);
+      below = (unsigned)__builtin_amdgcn_readlane((int)below, wl);
+      prefix |= (unsigned long long)found << shift;
+      mask |= 0xFFull << shift;
+      rem -= (int)below;
+      wave_lds_sync();  // the next pass rewrites the histogram
+      if (cnt == (unsigned)rem) {
+        // the crossing bucket is taken whole: every key up to the bucket's top is selected
+        lt_bound = (prefix | ((1ull << shift) - 1ull)) + 1ull;
+        rem = 0;
+        break;
+      }
+    }
+    if (rem) lt_bound = prefix;
+    // take every key < lt_bound and, after a full 8-pass descent, the first `rem` keys == prefix
+    // (the exact keep-th distance) in index order
+    double* sd = knn_sd[w];
+    int* ss = knn_ss[w];
+    int pos = 0, eq_left = rem;
+    const unsigned long long lt_lane = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int si = lane + 64 * i;
+      const bool valid = si < n;
+      const bool lt = valid && key[i] < lt_bound;
+      const bool eq = valid && key[i] == prefix;
+      const unsigned long long eqm = __ballot(eq);
+      const int eq_rank = __popcll(eqm & lt_lane);
+      const bool take_eq = eq && eq_rank < eq_left;
+      const bool take = lt || take_eq;
+      const unsigned long long tm = __ballot(take);
+      if (take) {
+        const int p = pos + __popcll(tm & lt_lane);
+        sd[p] = d[i];
+        ss[p] = si;
+      }
+      pos += __popcll(tm);
+      eq_left -= min(eq_left, __popcll(eqm));
+    }
+    wave_lds_sync();
+    double vd = 0.0;
+    int vs = 0, rank = 0;
+    if (lane < keep) {
+      vd = sd[lane];
+      vs = ss[lane];
+      for (int m = 0; m < keep; ++m) rank += lex_less(sd[m], ss[m], vd, vs);
+    }
+    wave_lds_sync();
+    if (lane < keep) {
+      sd[rank] = vd;
+      ss[rank] = vs;
+    }
+    wave_lds_sync();
+    if (lane + drop < keep) {
+      my_s = ss[lane + drop];
+      my_d = sd[lane + drop];
+    }
+  }
+#else
+  unsigned taken = 0;
   for (int t = 0; t < keep; ++t) {
     double bd = __builtin_inf();
     int bs = 0x7fffffff;
@@ -259,19 +376,11 @@ __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
       bool ok = s < n && !((taken >> i) & 1u);
       if (ok && lex_less(d[i], s, bd, bs)) { bd = d[i]; bs = s; }
     }
-#ifndef PST_KNN_SHFL
     wave_argmin(bd, bs);  // DPP row ops, no LDS round trips (6 % faster than __shfl_xor)
-#else
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      double od = __shfl_xor(bd, o, 64);
-      int os = __shfl_xor(bs, o, 64);
-      if (lex_less(od, os, bd, bs)) { bd = od; bs = os; }
-    }
-#endif
     if ((bs & 63) == lane) taken |= 1u << (bs >> 6);
     if (t - drop == lane) { my_s = bs; my_d = bd; }
   }
+#endif
   const int deg = n <= KNN ? n : KNN;
   if (lane == 0) a.deg[g] = deg;
   if (lane < KNN) {

@@ -117,6 +117,23 @@ def test_casp14_batch():
     _check_batch(samples, 4096, 1, layers=False)
 
 
+def _lattice_protein(side, seed):
+    """Identical residues translated onto a side^3 grid (4 A spacing, dyadic atom offsets): the
+    centroid distances repeat exactly, so the k-NN selection meets many exact ties at its cut."""
+    s = synthetic.synthetic_protein(side ** 3, seed)
+    ex = s.atom37_gt_exists[0]
+    off = np.round((s.atom37_positions[0] - s.atom37_positions[0, 1]) * 8) / 8
+    g = np.stack(np.meshgrid(*[np.arange(side)] * 3, indexing="ij"), -1).reshape(-1, 3) * 4.0
+    pos = g[:, None, :] + off[None]
+    gt = np.broadcast_to(ex, s.atom37_gt_exists.shape).copy()
+    return s._replace(atom37_positions=pos, atom37_gt_exists=gt, atom37_atom_exists=gt.copy())
+
+
+def test_distance_ties_lattice():
+    """Exact distance ties at the neighbour cut resolve to the lower index, as in the oracle."""
+    _check_batch([_lattice_protein(4, 2), _lattice_protein(7, 3), _lattice_protein(8, 4)], 4096, 1, layers=False)
+
+
 def test_size_gates_raise_like_reference():
     tk = tokenizer()
     with pytest.raises(NotImplementedError):
