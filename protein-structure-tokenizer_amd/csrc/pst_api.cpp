@@ -19,6 +19,8 @@ namespace {
 
 constexpr int H = 128;
 constexpr int KNN = 50;
+// split MPNN mode up to this many 32-receiver tasks (PST_SPLIT_TASKS overrides; measured in DESIGN.md)
+constexpr int64_t PST_SPLIT_TASKS_DEFAULT = 1024;
 
 thread_local std::string g_create_error;
 
@@ -215,6 +217,10 @@ struct pst_ctx {
   // grow-only scratch of pst_codebook_aux (host variant)
   void* aux = nullptr;
   size_t aux_bytes = 0;
+  // grow-only per-edge message rows of the split MPNN mode (small batches only)
+  float* msg = nullptr;
+  size_t msg_bytes = 0;
+  int64_t split_tasks = -1;  // split mode when n_tasks <= this (PST_SPLIT_TASKS; <0 = unset)
   std::vector<int64_t> h_offsets;
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
@@ -483,12 +489,39 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   auto mlp = [&](const MlpOff& o) {
     return pst::MlpW{F4(o.w0), A + o.b0, F4(o.w1), A + o.b1, F4(o.w2), A + o.b2, F4(o.bf1), F4(o.bf2)};
   };
+  // Small batches (n_tasks waves cannot fill 256 CUs x 8 wave slots) run each layer split in two
+  // launches, edge blocks spread over ~4096 waves, messages through HBM; bit-identical results.
+  const int64_t n_tasks = Rpad / 32;
+  if (ctx->split_tasks < 0) {
+    const char* e = getenv("PST_SPLIT_TASKS");
+    ctx->split_tasks = e ? std::max<int64_t>(0, atoll(e)) : PST_SPLIT_TASKS_DEFAULT;
+  }
+  float* msg_rows = nullptr;
+  int32_t bpw = 1;
+  if (n_tasks <= ctx->split_tasks) {
+    const size_t need = (size_t)n_tasks * 32 * KNN * 128 * sizeof(float);
+    if (need > ctx->msg_bytes) {
+      if (ctx->msg) (void)hipFree(ctx->msg);
+      ctx->msg = nullptr;
+      ctx->msg_bytes = 0;
+      hipError_t e = hipMalloc(&ctx->msg, need);
+      if (e != hipSuccess) {
+        ctx->msg = nullptr;
+        return fail(ctx, PST_E_NOMEM, std::string("message buffer allocation failed: ") + hipGetErrorString(e));
+      }
+      ctx->msg_bytes = need;
+    }
+    msg_rows = ctx->msg;
+    bpw = (int32_t)std::max<int64_t>(1, (n_tasks * 50 + 4095) / 4096);
+  }
   float* hbuf[4] = {nullptr, w.h0, w.h1, w.h0};
   float* ebuf[3] = {w.e0, w.e1, nullptr};
   float* pbuf[3] = {w.P0, w.P1, nullptr};
   for (int l = 0; l < 3; ++l) {
     pst::MpnnArgs m{};
-    m.n_tasks = Rpad / 32;
+    m.n_tasks = n_tasks;
+    m.msg_rows = msg_rows;
+    m.blocks_per_wave = bpw;
     m.senders = w.senders;
     m.deg = w.deg;
     m.node_local = w.node_local;
@@ -684,6 +717,7 @@ int pst_destroy(pst_ctx* ctx) {
   for (int i = 0; i <= PST_N_STAGES; ++i)
     if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
   if (ctx->aux) (void)hipFree(ctx->aux);
+  if (ctx->msg) (void)hipFree(ctx->msg);
   for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -76,6 +76,9 @@ struct MpnnArgs {
   const float4* ff_bf1;      // [4 chunks][64 lanes] float4 bias fragments
   const float4* ff_bf2;
   float* agg;  // [n_tasks][32][128] scratch: segment sums (perm order)
+  // split mode (k_mpnn_edge + k_mpnn_node) when non-null: per-edge messages [E][128] (perm rows)
+  float* msg_rows;
+  int32_t blocks_per_wave;  // edge blocks of 32 per k_mpnn_edge wave
   // outputs
   float* e_out;  // blocked (null for the last layer)
   float* h_out;

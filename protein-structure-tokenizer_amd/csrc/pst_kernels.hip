@@ -446,6 +446,127 @@ __device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
   tile_gemm_bf(acc, a2, W.w2, W.bf2, ActGelu{});
 }
 
+// One 32-edge block `blk` of task `task` (receivers g0 .. g0+31): for LAYER >= 1 the edge
+// update of layer LAYER-1, e = LN(e + MLP([h_s | h_r | e])), stored back blocked; for LAYER 0
+// the edge embedding. Then the message MLP of layer LAYER -> m.
+template <int LAYER>
+__device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int64_t g0, int lane, int blk, Tile& m) {
+  const int te = 32 * blk + (lane & 31);
+  const int rl = te / 50;
+  const int64_t g = g0 + rl;
+  const int64_t E = g * KNN + (te - 50 * rl);
+#ifdef PST_EXP_HOT_GATHER
+  const int64_t s = g;
+#else
+  const int64_t s = a.senders[E];
+#endif
+#ifdef PST_EXP_HOTE
+  const int64_t eblk = (task * 50) * 4096;
+#else
+  const int64_t eblk = (task * 50 + blk) * 4096;
+#endif
+  Tile e;
+  if (LAYER == 0) {
+    // init_edge_embed: chain from T[s-r] (= b + edgePE(s-r) W[0:128]) over the 27 (+5 zero) features
+    int lr = a.node_local[g], ls = a.node_local[s];
+    lr = lr < 0 ? 0 : lr;
+    ls = ls < 0 ? lr : ls;
+    tile_load_perm(e, a.Ttab + (int64_t)(ls - lr + 511) * 128);
+    const float4* fp = reinterpret_cast<const float4*>(a.feat + E * 32 + 4 * (lane >> 5));
+    float x[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 v = fp[2 * q];
+      x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+    }
+    const float4* wf = a.W_embed + lane;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float4 wa = wf[r * 64];
+      e.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, x[r], e.m[0], 0, 0, 0);
+      e.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, x[r], e.m[1], 0, 0, 0);
+      e.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, x[r], e.m[2], 0, 0, 0);
+      e.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, x[r], e.m[3], 0, 0, 0);
+    }
+  } else {
+    // edge update of layer LAYER-1: e = LN(e + MLP([h_s | h_r | e]))
+    Tile ein;
+    tile_load_blk(ein, a.e_in + eblk);
+    Tile acc;
+    tile_add_rows(acc, a.P_in + s * 512 + 0, a.P_in + g * 512 + 128);
+    mlp3(acc, ein, a.edge);
+    tile_load_blk(e, a.e_in + eblk);
+    tile_add(e, acc);
+#ifndef PST_EXP_NOLN
+    tile_layer_norm(e, a.edge_ln_s, a.edge_ln_o);
+#endif
+  }
+#ifndef PST_EXP_NOSTORE
+  if (a.e_out) tile_store_blk(e, a.e_out + eblk);
+#endif
+  // message MLP of layer LAYER
+  if (LAYER == 0) {
+    int lr = a.node_local[g], ls = a.node_local[s];
+    lr = lr < 0 ? 0 : lr;
+    ls = ls < 0 ? lr : ls;
+    tile_add_rows(m, a.PM0 + (int64_t)ls * 256 + 0, a.PM0 + (int64_t)lr * 256 + 128);
+  } else {
+    tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
+  }
+  mlp3(m, e, a.msg);
+}
+
+// Node update of the 32 receivers g0 .. g0+31 (lane&31 = receiver): x = h + agg/50, where
+// aggl holds the 32 ordered segment sums (perm rows); h = LN(x); h = LN(h + FFN(h)); then the
+// next layer's 4 node projections.
+template <int LAYER>
+__device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t g0, const float* aggl) {
+  const int64_t gl = g0 + (lane & 31);
+  Tile x;
+  {
+    Tile ag;
+    tile_load_perm(ag, aggl + (lane & 31) * 128);
+    if (LAYER == 0) {
+      int lr = a.node_local[gl];
+      tile_load_perm(x, a.h0tab + (int64_t)(lr < 0 ? 0 : lr) * 128);
+    } else {
+      tile_load_perm(x, a.h_in + gl * 128);
+    }
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x.m[M][r] = x.m[M][r] + ag.m[M][r] / 50.0f;
+  }
+  tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0
+  Tile out;
+  for (int ck = 0; ck < 4; ++ck) {
+    Tile hid;
+    tile_gemm_bf(hid, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, ActId{});
+    if (ck == 0)
+      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu{});
+    else
+      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu{});
+  }
+  tile_add(x, out);
+  tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
+  tile_store_perm(x, a.h_out + gl * 128);
+  if (a.P_out) {
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+      Tile pr;
+      if (p & 1) {  // receiver parts chain from the layer's first-layer bias
+        tile_gemm_bf(pr, x, a.proj_w + p * 64 * 64, a.proj_bf[p >> 1], ActId{});
+      } else {
+        tile_zero(pr);
+        tile_gemm(pr, x, a.proj_w + p * 64 * 64);
+      }
+      tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
+    }
+  }
+}
+
+// Fused layer (large batches): one wave per task runs its 50 edge blocks in order, carrying the
+// ordered segment sums in registers/LDS, then the node update. No per-edge message traffic.
 template <int LAYER>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   __shared__ float lds_scratch[4][32 * 36];
@@ -468,70 +589,8 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   float carry[4] = {0.f, 0.f, 0.f, 0.f};
 
   for (int blk = 0; blk < 50; ++blk) {
-    const int te = 32 * blk + (lane & 31);
-    const int rl = te / 50;
-    const int64_t g = g0 + rl;
-    const int64_t E = g * KNN + (te - 50 * rl);
-#ifdef PST_EXP_HOT_GATHER
-    const int64_t s = g;
-#else
-    const int64_t s = a.senders[E];
-#endif
-#ifdef PST_EXP_HOTE
-    const int64_t eblk = (task * 50) * 4096;
-#else
-    const int64_t eblk = (task * 50 + blk) * 4096;
-#endif
-    Tile e;
-    if (LAYER == 0) {
-      // init_edge_embed: chain from T[s-r] (= b + edgePE(s-r) W[0:128]) over the 27 (+5 zero) features
-      int lr = a.node_local[g], ls = a.node_local[s];
-      lr = lr < 0 ? 0 : lr;
-      ls = ls < 0 ? lr : ls;
-      tile_load_perm(e, a.Ttab + (int64_t)(ls - lr + 511) * 128);
-      const float4* fp = reinterpret_cast<const float4*>(a.feat + E * 32 + 4 * (lane >> 5));
-      float x[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 v = fp[2 * q];
-        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
-      }
-      const float4* wf = a.W_embed + lane;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float4 wa = wf[r * 64];
-        e.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, x[r], e.m[0], 0, 0, 0);
-        e.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, x[r], e.m[1], 0, 0, 0);
-        e.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, x[r], e.m[2], 0, 0, 0);
-        e.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, x[r], e.m[3], 0, 0, 0);
-      }
-    } else {
-      // edge update of layer LAYER-1: e = LN(e + MLP([h_s | h_r | e]))
-      Tile ein;
-      tile_load_blk(ein, a.e_in + eblk);
-      Tile acc;
-      tile_add_rows(acc, a.P_in + s * 512 + 0, a.P_in + g * 512 + 128);
-      mlp3(acc, ein, a.edge);
-      tile_load_blk(e, a.e_in + eblk);
-      tile_add(e, acc);
-#ifndef PST_EXP_NOLN
-      tile_layer_norm(e, a.edge_ln_s, a.edge_ln_o);
-#endif
-    }
-#ifndef PST_EXP_NOSTORE
-    if (a.e_out) tile_store_blk(e, a.e_out + eblk);
-#endif
-    // message MLP of layer LAYER
     Tile m;
-    if (LAYER == 0) {
-      int lr = a.node_local[g], ls = a.node_local[s];
-      lr = lr < 0 ? 0 : lr;
-      ls = ls < 0 ? lr : ls;
-      tile_add_rows(m, a.PM0 + (int64_t)ls * 256 + 0, a.PM0 + (int64_t)lr * 256 + 128);
-    } else {
-      tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
-    }
-    mlp3(m, e, a.msg);
+    edge_block<LAYER>(a, task, task * 32, lane, blk, m);
     // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order):
     // transpose through LDS, then each lane runs the sequential chain of its channel; lane
     // half 0 continues the receiver that owns edge 0 of the block (rA), half 1 starts rA+1.
@@ -579,7 +638,9 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  // ---------------- node update for the 32 receivers (lane&31 = receiver)
+  // ---------------- node update for the 32 receivers (lane&31 = receiver): the body of
+  // node_update, kept inline here — calling the helper makes the compiler spill 45 VGPRs
+  // in k_mpnn<1,2> (2 inline).
   const int64_t gl = g0 + (lane & 31);
   Tile x;
   {
@@ -622,6 +683,61 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
       tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
     }
   }
+}
+
+// Split layer (small batches, where one wave per 32 receivers cannot fill the GPU): the edge
+// blocks of all tasks run in parallel, `blocks_per_wave` consecutive blocks per wave, and store
+// their messages as rows `msg_rows[E][128]` (perm order); k_mpnn_node then forms each receiver's
+// ordered segment sum from those rows — the same additions in the same order as k_mpnn, so
+// both modes give identical bits.
+template <int LAYER>
+__global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_edge(MpnnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nb = a.n_tasks * 50;
+  const int64_t b0 = ((int64_t)blockIdx.x * 4 + w) * a.blocks_per_wave;
+  if (b0 >= nb) return;
+  const int64_t b1 = min(b0 + (int64_t)a.blocks_per_wave, nb);
+  for (int64_t gb = b0; gb < b1; ++gb) {
+    const int64_t task = gb / 50;
+    const int blk = (int)(gb - task * 50);
+    Tile m;
+    edge_block<LAYER>(a, task, task * 32, lane, blk, m);
+    tile_store_perm(m, a.msg_rows + (gb * 32 + (lane & 31)) * 128);  // row E = task*1600 + 32*blk + col
+  }
+}
+
+template <int LAYER>
+__global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_node(MpnnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t task = (int64_t)blockIdx.x * 4 + w;
+  if (task >= a.n_tasks) return;
+  const int64_t g0 = task * 32;
+  const int64_t gl = g0 + (lane & 31);
+  const int deg = a.deg[gl];
+  // agg = ((0 + m_0) + m_1) + ... + m_{deg-1}, per channel (this lane's 64 channels); each lane
+  // stores and re-reads only its own half row, so no barrier is needed
+  float* aggl = a.agg + task * 32 * 128;
+  {
+    Tile ag;
+    tile_zero(ag);
+    const float4* row = reinterpret_cast<const float4*>(a.msg_rows + gl * KNN * 128 + (lane >> 5) * 64);
+    for (int j = 0; j < deg; ++j) {
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = row[j * 32 + M * 4 + q];
+          ag.m[M][4 * q + 0] = ag.m[M][4 * q + 0] + v.x;
+          ag.m[M][4 * q + 1] = ag.m[M][4 * q + 1] + v.y;
+          ag.m[M][4 * q + 2] = ag.m[M][4 * q + 2] + v.z;
+          ag.m[M][4 * q + 3] = ag.m[M][4 * q + 3] + v.w;
+        }
+    }
+    tile_store_perm(ag, aggl + (lane & 31) * 128);
+  }
+  node_update<LAYER>(a, lane, g0, aggl);
 }
 
 // ---------------------------------------------------------------------------- k_down
@@ -855,6 +971,17 @@ void launch_knn(const KnnArgs& a, hipStream_t st) {
 }
 void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st) {
   dim3 grid((unsigned)((a.n_tasks + 3) / 4));
+  if (a.msg_rows) {  // split mode
+    const int64_t waves = (a.n_tasks * 50 + a.blocks_per_wave - 1) / a.blocks_per_wave;
+    dim3 egrid((unsigned)((waves + 3) / 4));
+    if (layer == 0) hipLaunchKernelGGL(k_mpnn_edge<0>, egrid, dim3(256), 0, st, a);
+    else if (layer == 1) hipLaunchKernelGGL(k_mpnn_edge<1>, egrid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_mpnn_edge<2>, egrid, dim3(256), 0, st, a);
+    if (layer == 0) hipLaunchKernelGGL(k_mpnn_node<0>, grid, dim3(256), 0, st, a);
+    else if (layer == 1) hipLaunchKernelGGL(k_mpnn_node<1>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_mpnn_node<2>, grid, dim3(256), 0, st, a);
+    return;
+  }
   if (layer == 0) hipLaunchKernelGGL(k_mpnn<0>, grid, dim3(256), 0, st, a);
   else if (layer == 1) hipLaunchKernelGGL(k_mpnn<1>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(k_mpnn<2>, grid, dim3(256), 0, st, a);
