@@ -106,6 +106,99 @@ __device__ __forceinline__ f32x2 c_gelu2(f32x2 x) {
   return pk_fma(hx, t, hx);
 }
 
+// c_gelu2 with every packed op pinned as v_pk_* by inline asm: the compiler's pre-emit peephole
+// otherwise unpacks packed FP32 ops that sit in an MFMA's shadow into two scalar ops each, and on
+// gfx950 that costs VALU issue cycles the MFMA pipe does not hide (A/B on the box: k_mpnn 1.8 %
+// faster pinned; PMC SQ_VALU_MFMA_COEXEC_CYCLES = 0). Same op sequence as c_gelu2, bit for bit.
+// Constant operands: SGPR pairs holding the constant in both halves (sc2).
+__device__ __forceinline__ uint64_t sc2(float c) { return (uint64_t)__float_as_uint(c) * 0x100000001ull; }
+__device__ __forceinline__ f32x2 apk_mul(f32x2 a, f32x2 b) {
+  f32x2 d;
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ f32x2 apk_mul_s(f32x2 a, uint64_t c) {
+  f32x2 d;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(d) : "v"(a), "s"(c));
+  return d;
+}
+// a*b + c, c an SGPR constant
+__device__ __forceinline__ f32x2 apk_fma_vvs(f32x2 a, f32x2 b, uint64_t c) {
+  f32x2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+}
+// a*b + c, b an SGPR constant, c a VGPR pair
+__device__ __forceinline__ f32x2 apk_fma_vsv(f32x2 a, uint64_t b, f32x2 c) {
+  f32x2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "s"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ f32x2 apk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  f32x2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+// -a*b + c
+__device__ __forceinline__ f32x2 apk_fma_neg(f32x2 a, f32x2 b, f32x2 c) {
+  f32x2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+// FRESH: x may have been written by an MFMA only a few instructions ago. Only the compiler's
+// hazard recognizer knows the wait states an MFMA-written VGPR needs before a VALU read (an asm
+// read can see the accumulator before its last k-step), so then the first step stays in C.
+// tile_gemm_f evaluates k-steps 0..3 right after the producing GEMM (FRESH); later k-steps read
+// accumulators finished >= 4 MFMA groups earlier. The clamp and the reciprocal stay in C (no
+// packed forms); the s_nop covers the v_rcp (trans) result-forwarding hazard, which the
+// recognizer does not check for asm operands.
+template <bool FRESH>
+__device__ __forceinline__ f32x2 c_gelu2_asm(f32x2 x) {
+  const f32x2 c5 = splat2(2.00018790482477e-13f), q2 = splat2(1.18534705686654e-04f);
+  f32x2 u;
+  if (FRESH) {
+    u = x * pk_fma(x * x, splat2(GELU_K0K1), splat2(GELU_K0));
+  } else {
+    const f32x2 k0 = splat2(GELU_K0);
+    f32x2 t0;
+    asm("v_pk_mul_f32 %1, %2, %2\n\t"
+        "v_pk_fma_f32 %1, %1, %3, %4\n\t"
+        "v_pk_mul_f32 %0, %2, %1"
+        : "=&v"(u), "=&v"(t0)
+        : "v"(x), "s"(sc2(GELU_K0K1)), "v"(k0));
+  }
+  const float cl = 7.99881172180175781f;
+  f32x2 xc = {__builtin_amdgcn_fmed3f(u.x, -cl, cl), __builtin_amdgcn_fmed3f(u.y, -cl, cl)};
+  f32x2 p, q, sq;
+  asm("v_pk_mul_f32 %2, %3, %3\n\t"
+      "v_pk_fma_f32 %0, %2, %4, %5\n\t"
+      "v_pk_fma_f32 %0, %2, %0, %6\n\t"
+      "v_pk_fma_f32 %0, %2, %0, %7\n\t"
+      "v_pk_fma_f32 %0, %2, %0, %8\n\t"
+      "v_pk_fma_f32 %0, %2, %0, %9\n\t"
+      "v_pk_fma_f32 %0, %2, %0, %10\n\t"
+      "v_pk_mul_f32 %0, %3, %0\n\t"
+      "v_pk_fma_f32 %1, %2, %11, %12\n\t"
+      "v_pk_fma_f32 %1, %2, %1, %13\n\t"
+      "v_pk_fma_f32 %1, %2, %1, %14"
+      : "=&v"(p), "=&v"(q), "=&v"(sq)
+      : "v"(xc), "s"(sc2(-2.76076847742355e-16f)), "v"(c5), "s"(sc2(-8.60467152213735e-11f)),
+        "s"(sc2(5.12229709037114e-08f)), "s"(sc2(1.48572235717979e-05f)), "s"(sc2(6.37261928875436e-04f)),
+        "s"(sc2(4.89352455891786e-03f)), "s"(sc2(1.19825839466702e-06f)), "v"(q2),
+        "s"(sc2(2.26843463243900e-03f)), "s"(sc2(4.89352518554385e-03f)));
+  f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+  f32x2 out, y, e, t, hx;
+  asm("s_nop 0\n\t"
+      "v_pk_mul_f32 %1, %5, %6\n\t"
+      "v_pk_fma_f32 %2, %7, %1, %5 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+      "v_pk_fma_f32 %3, %2, %6, %1\n\t"
+      "v_pk_mul_f32 %4, %8, %9\n\t"
+      "v_pk_fma_f32 %0, %4, %3, %4"
+      : "=&v"(out), "=&v"(y), "=&v"(e), "=&v"(t), "=&v"(hx)
+      : "v"(p), "v"(r), "v"(q), "v"(x), "s"(sc2(0.5f)));
+  return out;
+}
+
 __device__ __forceinline__ float c_ldexpf(float v, int n) {
   if (n < -126) {
     v = v * __uint_as_float((uint32_t)(-126 + 127) << 23);
@@ -335,7 +428,15 @@ struct ActId {
 // GELU of the previous layer's output (its bias is already in the accumulator: chains start
 // from the bias)
 struct ActGelu {
+#ifdef PST_SCALAR_GELU
+  __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return (f32x2){c_gelu(x.x), c_gelu(x.y)}; }
+#elif defined(PST_C_GELU)
   __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return c_gelu2(x); }
+#else
+  __device__ __forceinline__ f32x2 operator()(int t, f32x2 x) const {
+    return t < 4 ? c_gelu2_asm<true>(x) : c_gelu2_asm<false>(x);
+  }
+#endif
 };
 
 struct ActBiasRelu {
