@@ -150,8 +150,8 @@ __device__ __forceinline__ f32x2 apk_fma_neg(f32x2 a, f32x2 b, f32x2 c) {
 // read can see the accumulator before its last k-step), so then the first step stays in C.
 // tile_gemm_f evaluates k-steps 0..3 right after the producing GEMM (FRESH); later k-steps read
 // accumulators finished >= 4 MFMA groups earlier. The clamp and the reciprocal stay in C (no
-// packed forms); the s_nop covers the v_rcp (trans) result-forwarding hazard, which the
-// recognizer does not check for asm operands.
+// packed forms). Measured costs (A/B, 512 x 256 residues): the GELU is ~10 % of k_mpnn, since
+// f32 MFMA and f32 VALU share the vector datapath (MI355X: f32 MFMA peak = vector peak).
 template <bool FRESH>
 __device__ __forceinline__ f32x2 c_gelu2_asm(f32x2 x) {
   const f32x2 c5 = splat2(2.00018790482477e-13f), q2 = splat2(1.18534705686654e-04f);
@@ -169,33 +169,35 @@ __device__ __forceinline__ f32x2 c_gelu2_asm(f32x2 x) {
   }
   const float cl = 7.99881172180175781f;
   f32x2 xc = {__builtin_amdgcn_fmed3f(u.x, -cl, cl), __builtin_amdgcn_fmed3f(u.y, -cl, cl)};
-  f32x2 p, q, sq;
-  asm("v_pk_mul_f32 %2, %3, %3\n\t"
-      "v_pk_fma_f32 %0, %2, %4, %5\n\t"
-      "v_pk_fma_f32 %0, %2, %0, %6\n\t"
-      "v_pk_fma_f32 %0, %2, %0, %7\n\t"
-      "v_pk_fma_f32 %0, %2, %0, %8\n\t"
-      "v_pk_fma_f32 %0, %2, %0, %9\n\t"
-      "v_pk_fma_f32 %0, %2, %0, %10\n\t"
-      "v_pk_mul_f32 %0, %3, %0\n\t"
-      "v_pk_fma_f32 %1, %2, %11, %12\n\t"
-      "v_pk_fma_f32 %1, %2, %1, %13\n\t"
-      "v_pk_fma_f32 %1, %2, %1, %14"
-      : "=&v"(p), "=&v"(q), "=&v"(sq)
-      : "v"(xc), "s"(sc2(-2.76076847742355e-16f)), "v"(c5), "s"(sc2(-8.60467152213735e-11f)),
-        "s"(sc2(5.12229709037114e-08f)), "s"(sc2(1.48572235717979e-05f)), "s"(sc2(6.37261928875436e-04f)),
-        "s"(sc2(4.89352455891786e-03f)), "s"(sc2(1.19825839466702e-06f)), "v"(q2),
-        "s"(sc2(2.26843463243900e-03f)), "s"(sc2(4.89352518554385e-03f)));
+  f32x2 q, sq;
+  asm("v_pk_mul_f32 %1, %2, %2\n\t"
+      "v_pk_fma_f32 %0, %1, %3, %4\n\t"
+      "v_pk_fma_f32 %0, %1, %0, %5\n\t"
+      "v_pk_fma_f32 %0, %1, %0, %6"
+      : "=&v"(q), "=&v"(sq)
+      : "v"(xc), "s"(sc2(1.19825839466702e-06f)), "v"(q2), "s"(sc2(2.26843463243900e-03f)),
+        "s"(sc2(4.89352518554385e-03f)));
+  // the reciprocal issues here, 7 instructions before its first use in the next group: that
+  // covers the one wait state a v_rcp (trans) result needs, which the hazard recognizer does
+  // not check for asm operands
   f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
-  f32x2 out, y, e, t, hx;
-  asm("s_nop 0\n\t"
-      "v_pk_mul_f32 %1, %5, %6\n\t"
-      "v_pk_fma_f32 %2, %7, %1, %5 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-      "v_pk_fma_f32 %3, %2, %6, %1\n\t"
-      "v_pk_mul_f32 %4, %8, %9\n\t"
-      "v_pk_fma_f32 %0, %4, %3, %4"
-      : "=&v"(out), "=&v"(y), "=&v"(e), "=&v"(t), "=&v"(hx)
-      : "v"(p), "v"(r), "v"(q), "v"(x), "s"(sc2(0.5f)));
+  f32x2 out, p, y, e, t, hx;
+  asm("v_pk_fma_f32 %1, %7, %10, %11\n\t"
+      "v_pk_fma_f32 %1, %7, %1, %12\n\t"
+      "v_pk_fma_f32 %1, %7, %1, %13\n\t"
+      "v_pk_fma_f32 %1, %7, %1, %14\n\t"
+      "v_pk_fma_f32 %1, %7, %1, %15\n\t"
+      "v_pk_fma_f32 %1, %7, %1, %16\n\t"
+      "v_pk_mul_f32 %1, %6, %1\n\t"
+      "v_pk_mul_f32 %2, %1, %8\n\t"
+      "v_pk_fma_f32 %3, %9, %2, %1 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+      "v_pk_fma_f32 %4, %3, %8, %2\n\t"
+      "v_pk_mul_f32 %5, %17, %18\n\t"
+      "v_pk_fma_f32 %0, %5, %4, %5"
+      : "=&v"(out), "=&v"(p), "=&v"(y), "=&v"(e), "=&v"(t), "=&v"(hx)
+      : "v"(xc), "v"(sq), "v"(r), "v"(q), "s"(sc2(-2.76076847742355e-16f)), "v"(c5),
+        "s"(sc2(-8.60467152213735e-11f)), "s"(sc2(5.12229709037114e-08f)), "s"(sc2(1.48572235717979e-05f)),
+        "s"(sc2(6.37261928875436e-04f)), "s"(sc2(4.89352455891786e-03f)), "v"(x), "s"(sc2(0.5f)));
   return out;
 }
 
@@ -428,7 +430,9 @@ struct ActId {
 // GELU of the previous layer's output (its bias is already in the accumulator: chains start
 // from the bias)
 struct ActGelu {
-#ifdef PST_SCALAR_GELU
+#if defined(PST_EXP_NOGELU)  // ablation: identity (results differ; timing only)
+  __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return x; }
+#elif defined(PST_SCALAR_GELU)
   __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return (f32x2){c_gelu(x.x), c_gelu(x.y)}; }
 #elif defined(PST_C_GELU)
   __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return c_gelu2(x); }

@@ -449,17 +449,27 @@ __device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
 // One 32-edge block `blk` of task `task` (receivers g0 .. g0+31): for LAYER >= 1 the edge
 // update of layer LAYER-1, e = LN(e + MLP([h_s | h_r | e])), stored back blocked; for LAYER 0
 // the edge embedding. Then the message MLP of layer LAYER -> m.
+// Sender of this lane's edge in 32-edge block `blk` of the task starting at receiver g0. The
+// callers load it one block ahead: the sender index heads a chain of dependent loads (index →
+// projection rows), so fetching it during the previous block's GEMMs takes one memory latency
+// off every block.
+__device__ __forceinline__ int32_t edge_sender(const MpnnArgs& a, int64_t g0, int lane, int blk) {
+#ifdef PST_EXP_HOT_GATHER
+  const int te = 32 * blk + (lane & 31);
+  return (int32_t)(g0 + te / 50);
+#else
+  return a.senders[g0 * KNN + 32 * blk + (lane & 31)];
+#endif
+}
+
 template <int LAYER>
-__device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int64_t g0, int lane, int blk, Tile& m) {
+__device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int64_t g0, int lane, int blk,
+                                           int32_t s_pre, Tile& m) {
   const int te = 32 * blk + (lane & 31);
   const int rl = te / 50;
   const int64_t g = g0 + rl;
   const int64_t E = g * KNN + (te - 50 * rl);
-#ifdef PST_EXP_HOT_GATHER
-  const int64_t s = g;
-#else
-  const int64_t s = a.senders[E];
-#endif
+  const int64_t s = s_pre;
 #ifdef PST_EXP_HOTE
   const int64_t eblk = (task * 50) * 4096;
 #else
@@ -588,9 +598,12 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   const int c = lane & 31, part = lane >> 5;
   float carry[4] = {0.f, 0.f, 0.f, 0.f};
 
+  int32_t s_next = edge_sender(a, g0, lane, 0);
   for (int blk = 0; blk < 50; ++blk) {
+    const int32_t s_cur = s_next;
+    if (blk < 49) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
-    edge_block<LAYER>(a, task, task * 32, lane, blk, m);
+    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m);
     // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order):
     // transpose through LDS, then each lane runs the sequential chain of its channel; lane
     // half 0 continues the receiver that owns edge 0 of the block (rA), half 1 starts rA+1.
@@ -690,6 +703,8 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 // their messages as rows `msg_rows[E][128]` (perm order); k_mpnn_node then forms each receiver's
 // ordered segment sum from those rows — the same additions in the same order as k_mpnn, so
 // both modes give identical bits.
+__device__ __forceinline__ int64_t gb_edge(int64_t gb, int lane) { return gb * 32 + (lane & 31); }
+
 template <int LAYER>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_edge(MpnnArgs a) {
   const int lane = threadIdx.x & 63;
@@ -698,11 +713,15 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_edge(MpnnArgs a) 
   const int64_t b0 = ((int64_t)blockIdx.x * 4 + w) * a.blocks_per_wave;
   if (b0 >= nb) return;
   const int64_t b1 = min(b0 + (int64_t)a.blocks_per_wave, nb);
+  // edge block gb covers edges 32*gb .. 32*gb+31 (E = task*1600 + 32*blk + col)
+  int32_t s_next = a.senders[gb_edge(b0, lane)];
   for (int64_t gb = b0; gb < b1; ++gb) {
     const int64_t task = gb / 50;
     const int blk = (int)(gb - task * 50);
+    const int32_t s_cur = s_next;
+    if (gb + 1 < b1) s_next = a.senders[gb_edge(gb + 1, lane)];
     Tile m;
-    edge_block<LAYER>(a, task, task * 32, lane, blk, m);
+    edge_block<LAYER>(a, task, task * 32, lane, blk, s_cur, m);
     tile_store_perm(m, a.msg_rows + (gb * 32 + (lane & 31)) * 128);  // row E = task*1600 + 32*blk + col
   }
 }
