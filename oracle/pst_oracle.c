@@ -420,15 +420,31 @@ typedef struct {
 
 /* Every Linear's fma chain starts from its bias ("bias-first"); the first layer of an edge
  * MLP starts from Ps[s] + Pr[r], where Pr's own chain started from that layer's bias. */
-static void mlp3(const float* Ps, const float* Pr, const float* e, const lin_t* L, int act_last, float* y) {
-  float init[H], t1[H], t2[H];
-  for (int c = 0; c < H; ++c) init[c] = Ps[c] + Pr[c];
-  gemv(e, H, L[0].w + 2 * H * H, H, H, init, NULL, t1);
+static void mlp3_tail(float* t1, const lin_t* L, float* y) {
+  float t2[H];
   for (int c = 0; c < H; ++c) t1[c] = c_gelu(t1[c]);
   gemv(t1, H, L[1].w, H, H, L[1].b, NULL, t2);
   for (int c = 0; c < H; ++c) t2[c] = c_gelu(t2[c]);
   gemv(t2, H, L[2].w, H, H, L[2].b, NULL, y);
-  (void)act_last;
+}
+
+static void mlp3(const float* Ps, const float* Pr, const float* e, const lin_t* L, float* y) {
+  float init[H], t1[H];
+  for (int c = 0; c < H; ++c) init[c] = Ps[c] + Pr[c];
+  gemv(e, H, L[0].w + 2 * H * H, H, H, init, NULL, t1);
+  mlp3_tail(t1, L, y);
+}
+
+/* Layer 0's message MLP through the factors of the edge embedding: with
+ * e0 = T[s-r] + f·Wf, the first layer's e-part is U[s-r] + f·Wm, U = T·Wc, Wm = Wf·Wc (Wc = the
+ * first layer's rows 256..383), each an fmaf chain in the canonical order; the chain starts from
+ * (Ps[s] + Pr[r]) + U[s-r] and runs over the 32 (27 + zero pad) features. */
+static void mlp3_l0(const float* Ps, const float* Pr, const float* U, const float* f32, const float* Wm,
+                    const lin_t* L, float* y) {
+  float init[H], t1[H];
+  for (int c = 0; c < H; ++c) init[c] = (Ps[c] + Pr[c]) + U[c];
+  gemv(f32, 32, Wm, H, H, init, NULL, t1);
+  mlp3_tail(t1, L, y);
 }
 
 /* node projections of an MLP's first layer: Ps = h W[0:128] (from 0), Pr = b + h W[128:256] */
@@ -478,6 +494,12 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
       for (int c = 27; c < 32; ++c) f32[c] = 0.0f;
       gemv(f32, 32, Wf, H, H, Ttab + (size_t)(s - r + 511) * H, NULL, e + slot * H);
     }
+  /* layer-0 message factors: U[x] = T[x]·Wc, Wm[f] = Wf[f]·Wc (rows 27..31 stay zero) */
+  const float* Wc = P.L[0].msg[0].w + 2 * H * H;
+  float* Utab = (float*)malloc(sizeof(float) * 1023 * H);
+  for (int x = 0; x < 1023; ++x) gemv(Ttab + (size_t)x * H, H, Wc, H, H, NULL, NULL, Utab + (size_t)x * H);
+  float* Wm = (float*)calloc(32 * H, sizeof(float));
+  for (int f = 0; f < 27; ++f) gemv(Wf + (size_t)f * H, H, Wc, H, H, NULL, NULL, Wm + (size_t)f * H);
   free(Ttab);
   free(Wf);
   for (int l = 0; l < 3; ++l) {
@@ -490,7 +512,7 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
           size_t slot = (size_t)r * k + j;
           int s = senders[slot] < 0 ? r : senders[slot];
           float m[H], x[H];
-          mlp3(Es + (size_t)s * H, Er + (size_t)r * H, e + slot * H, Mp->edge, 0, m);
+          mlp3(Es + (size_t)s * H, Er + (size_t)r * H, e + slot * H, Mp->edge, m);
           for (int c = 0; c < H; ++c) x[c] = e[slot * H + c] + m[c];
           layer_norm(x, Mp->ln_s[2], Mp->ln_o[2], en + slot * H);
         }
@@ -503,7 +525,14 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
       for (int j = 0; j < deg[r]; ++j) {
         size_t slot = (size_t)r * k + j;
         int s = senders[slot];
-        mlp3(Ps + (size_t)s * H, Pr + (size_t)r * H, e + slot * H, M->msg, 0, m);
+        if (l == 0) {
+          float f32[32];
+          memcpy(f32, feat + slot * 32, sizeof(f32));
+          for (int c = 27; c < 32; ++c) f32[c] = 0.0f;
+          mlp3_l0(Ps + (size_t)s * H, Pr + (size_t)r * H, Utab + (size_t)(s - r + 511) * H, f32, Wm, M->msg, m);
+        } else {
+          mlp3(Ps + (size_t)s * H, Pr + (size_t)r * H, e + slot * H, M->msg, m);
+        }
         for (int c = 0; c < H; ++c) agg[c] = agg[c] + m[c];
       }
       for (int c = 0; c < H; ++c) x[c] = h[(size_t)r * H + c] + agg[c] / 50.0f;
@@ -610,7 +639,7 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
     }
     tokens[t] = idx;
   }
-  free(h); free(hn); free(e); free(en); free(Ps); free(Pr); free(Es); free(Er);
+  free(h); free(hn); free(e); free(en); free(Ps); free(Pr); free(Es); free(Er); free(Utab); free(Wm);
   return T;
 }
 

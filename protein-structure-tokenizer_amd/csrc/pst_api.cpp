@@ -25,6 +25,8 @@ constexpr int64_t PST_SPLIT_TASKS_DEFAULT = 1024;
 thread_local std::string g_create_error;
 
 int tile_channel(int h, int M, int r) { return 32 * M + (r & 3) + 8 * (r >> 2) + 4 * h; }
+// canonical k order of every fmaf chain (0,4,1,5,2,6,3,7 per block of 8; oracle/pst_oracle.c pi8)
+int pi8(int t) { return (t & ~7) | ((t >> 1) & 3) | ((t & 1) << 2); }
 
 // ------------------------------------------------------------------ parameter views
 struct Lin {
@@ -182,13 +184,13 @@ struct pst_ctx {
   std::string err;
   // weights arena (device) + offsets
   float* d_arena = nullptr;
-  size_t emb_w = 0, emb_b = 0;
+  size_t emb_w = 0, emb_b = 0, w_msg0f = 0;
   LayerOff L[3]{};
   size_t proj[2]{};
   BlockOff B[3]{};
   size_t down_w = 0, down_b = 0;
   // tables (device, separate allocations)
-  float *d_h0 = nullptr, *d_PM0 = nullptr, *d_T = nullptr, *d_RPE = nullptr;
+  float *d_h0 = nullptr, *d_PM0 = nullptr, *d_T = nullptr, *d_U = nullptr, *d_RPE = nullptr;
   float fsq_half[8]{}, fsq_off[8]{}, fsq_shift[8]{};
   int fsq_L[8]{}, fsq_basis[8]{};
   // workspace (grow-only)
@@ -255,6 +257,25 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   Arena A;
   ctx->emb_w = A.add(frag(P.edge_embed.w, H, 128, 27, 32, 0, 128));
   ctx->emb_b = A.add(perm(P.edge_embed.b));
+  {
+    // layer-0 message over the embedding's feature factor: Wm[f] = Wf[f] · msg0
+    // W[256:384], each output an fmaf chain over the 128 channels in the canonical k order (the
+    // oracle computes the same chain)
+    const float* Wc = P.L[0].msg[0].w + (size_t)256 * H;
+    std::vector<float> Wm((size_t)32 * H, 0.0f);
+    for (int f = 0; f < 27; ++f) {
+      const float* wf = P.edge_embed.w + (size_t)(128 + f) * H;
+      for (int o = 0; o < H; ++o) {
+        float acc = 0.0f;
+        for (int t = 0; t < H; ++t) {
+          const int k = pi8(t);
+          acc = std::fmaf(wf[k], Wc[(size_t)k * H + o], acc);
+        }
+        Wm[(size_t)f * H + o] = acc;
+      }
+    }
+    ctx->w_msg0f = A.add(frag(Wm.data(), H, 0, 27, 32, 0, 128));
+  }
   for (int l = 0; l < 3; ++l) {
     const Layer& S = P.L[l];
     LayerOff& O = ctx->L[l];
@@ -349,6 +370,7 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   HIPCHK(hipMalloc(&ctx->d_h0, 512 * 128 * sizeof(float)));
   HIPCHK(hipMalloc(&ctx->d_PM0, 512 * 256 * sizeof(float)));
   HIPCHK(hipMalloc(&ctx->d_T, 1023 * 128 * sizeof(float)));
+  HIPCHK(hipMalloc(&ctx->d_U, 1023 * 128 * sizeof(float)));
   HIPCHK(hipMalloc(&ctx->d_RPE, (size_t)ctx->max_out * 128 * sizeof(float)));
   HIPCHK(hipMemcpy(ctx->d_RPE, rpe.data(), rpe.size() * sizeof(float), hipMemcpyHostToDevice));
   float* a = ctx->d_arena;
@@ -359,6 +381,8 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   pst::launch_table_gemm(ctx->d_h0, 512, F4(o_m0s), nullptr, nullptr, ctx->d_PM0, 256, ctx->stream);
   pst::launch_table_gemm(ctx->d_h0, 512, F4(o_m0r), nullptr, a + ctx->L[0].msg.b0, ctx->d_PM0 + 128, 256, ctx->stream);
   pst::launch_table_gemm(a + o_epe, 1023, F4(o_ee_w), nullptr, a + ctx->emb_b, ctx->d_T, 128, ctx->stream);
+  // U = T · msg0 W[256:384]: the edge-PE half of layer 0's message first layer
+  pst::launch_table_gemm(ctx->d_T, 1023, F4(ctx->L[0].msg.w0), nullptr, nullptr, ctx->d_U, 128, ctx->stream);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(ctx->stream));
   // FSQ constants (quantize.py:175-181, computed in float32 as JAX does)
@@ -531,6 +555,8 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.W_embed = F4(ctx->emb_w);
     m.b_embed = A + ctx->emb_b;
     m.PM0 = ctx->d_PM0;
+    m.Utab = ctx->d_U;
+    m.W_msg0f = F4(ctx->w_msg0f);
     m.h0tab = ctx->d_h0;
     if (l > 0) {
       m.e_in = ebuf[l - 1];
@@ -718,7 +744,7 @@ int pst_destroy(pst_ctx* ctx) {
     if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
   if (ctx->aux) (void)hipFree(ctx->aux);
   if (ctx->msg) (void)hipFree(ctx->msg);
-  for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_RPE, ctx->ws})
+  for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_U, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -53,6 +53,8 @@ struct MpnnArgs {
   const float4* W_embed;   // [16][64] float4: init_edge_embed rows 128..154 (+zero pad)
   const float* b_embed;    // perm (folded into Ttab: unused by the kernel)
   const float* PM0;        // [512][256] perm: h0 · msg0 W[0:128] | W[128:256]
+  const float* Utab;       // [1023][128] perm: T · msg0 W[256:384] (layer-0 message)
+  const float4* W_msg0f;   // [16][64] float4: init_edge_embed rows 128..154 · msg0 W[256:384]
   const float* h0tab;      // [512][128] perm: init_node_embed(node PE)
   // layers >= 1
   const float* e_in;       // blocked edge features of the previous layer

@@ -436,14 +436,46 @@ __device__ __forceinline__ void tile_add_rows(Tile& acc, const float* __restrict
     }
 }
 
+// acc += row (perm order), elementwise
+__device__ __forceinline__ void tile_add_row(Tile& acc, const float* __restrict__ row) {
+  const float4* p = reinterpret_cast<const float4*>(row + (lane_id() >> 5) * 64);
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 v = p[M * 4 + q];
+      acc.m[M][4 * q + 0] = acc.m[M][4 * q + 0] + v.x;
+      acc.m[M][4 * q + 1] = acc.m[M][4 * q + 1] + v.y;
+      acc.m[M][4 * q + 2] = acc.m[M][4 * q + 2] + v.z;
+      acc.m[M][4 * q + 3] = acc.m[M][4 * q + 3] + v.w;
+    }
+}
+
 // 3-layer edge MLP starting from acc = init (Ps[s] + Pr[r], Pr's chain started from b0):
 // acc <- MLP(init, X). Layers 2 and 3 chain from their biases; the GELU of layers 1 and 2 is
 // applied just in time inside the next GEMM.
-__device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
-  tile_gemm(acc, X, W.w0);
+__device__ __forceinline__ void mlp3_tail(Tile& acc, const MlpW& W) {
   Tile a2;
   tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu{});
   tile_gemm_bf(acc, a2, W.w2, W.bf2, ActGelu{});
+}
+__device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
+  tile_gemm(acc, X, W.w0);
+  mlp3_tail(acc, W);
+}
+
+// acc += x[features] · Wf over the 32 (27 + zero pad) edge features, 16 MFMA k-steps;
+// x[r] holds features (r&3) + 8(r>>2) + 4·half (the k order of the fragments)
+__device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const float4* __restrict__ Wf) {
+  const float4* wf = Wf + lane_id();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float4 wa = wf[r * 64];
+    acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, x[r], acc.m[0], 0, 0, 0);
+    acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, x[r], acc.m[1], 0, 0, 0);
+    acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, x[r], acc.m[2], 0, 0, 0);
+    acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, x[r], acc.m[3], 0, 0, 0);
+  }
 }
 
 // One 32-edge block `blk` of task `task` (receivers g0 .. g0+31): for LAYER >= 1 the edge
@@ -476,28 +508,23 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
   const int64_t eblk = (task * 50 + blk) * 4096;
 #endif
   Tile e;
+  float x[16];  // layer 0: this lane's edge features
+  int lr0 = 0, ls0 = 0;
   if (LAYER == 0) {
     // init_edge_embed: chain from T[s-r] (= b + edgePE(s-r) W[0:128]) over the 27 (+5 zero) features
     int lr = a.node_local[g], ls = a.node_local[s];
     lr = lr < 0 ? 0 : lr;
     ls = ls < 0 ? lr : ls;
+    lr0 = lr;
+    ls0 = ls;
     tile_load_perm(e, a.Ttab + (int64_t)(ls - lr + 511) * 128);
     const float4* fp = reinterpret_cast<const float4*>(a.feat + E * 32 + 4 * (lane >> 5));
-    float x[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float4 v = fp[2 * q];
       x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
     }
-    const float4* wf = a.W_embed + lane;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float4 wa = wf[r * 64];
-      e.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, x[r], e.m[0], 0, 0, 0);
-      e.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, x[r], e.m[1], 0, 0, 0);
-      e.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, x[r], e.m[2], 0, 0, 0);
-      e.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, x[r], e.m[3], 0, 0, 0);
-    }
+    feat_gemm(e, x, a.W_embed);
   } else {
     // edge update of layer LAYER-1: e = LN(e + MLP([h_s | h_r | e]))
     Tile ein;
@@ -516,14 +543,17 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
 #endif
   // message MLP of layer LAYER
   if (LAYER == 0) {
-    int lr = a.node_local[g], ls = a.node_local[s];
-    lr = lr < 0 ? 0 : lr;
-    ls = ls < 0 ? lr : ls;
-    tile_add_rows(m, a.PM0 + (int64_t)ls * 256 + 0, a.PM0 + (int64_t)lr * 256 + 128);
+    // first layer through the embedding's factors: e0·W = T[s-r]·W + f·(Wf·W),
+    // so the chain starts from (h_s·W_s + (b + h_r·W_r)) + U[s-r] and runs over the 32
+    // features: 16 k-steps instead of 64
+    tile_add_rows(m, a.PM0 + (int64_t)ls0 * 256 + 0, a.PM0 + (int64_t)lr0 * 256 + 128);
+    tile_add_row(m, a.Utab + (int64_t)(ls0 - lr0 + 511) * 128);
+    feat_gemm(m, x, a.W_msg0f);
+    mlp3_tail(m, a.msg);
   } else {
     tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
+    mlp3(m, e, a.msg);
   }
-  mlp3(m, e, a.msg);
 }
 
 // Node update of the 32 receivers g0 .. g0+31 (lane&31 = receiver): x = h + agg/50, where
