@@ -791,7 +791,9 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_node(MpnnArgs a) 
 
 // ---------------------------------------------------------------------------- k_down
 template <int DF>
-__global__ __launch_bounds__(256) void k_down(DownArgs a) {
+// df 1 fits 2 waves/SIMD in 256 registers (3 spilled); df 2/4 keep the attention state of DF
+// keys and need the 512-register, 1 wave/SIMD form
+__global__ __launch_bounds__(256, DF == 1 ? 2 : 1) void k_down(DownArgs a) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile_id = blockIdx.x * 4 + w;
