@@ -119,6 +119,25 @@ int pst_tokenize_device(pst_ctx* ctx, const double* d_atom_pos, const uint8_t* d
                         int32_t* d_n_tokens_out, int32_t* d_n_nodes_out);
 
 /*
+ * The residue graph alone (replaces the graph part of preprocessing.py:42-283
+ * preprocess_sample, i.e. protein_utils.py:325-438 compute_nearest_neighbors_graph on the
+ * residues with N, CA, C and O): runs the graph kernels of pst_tokenize and copies back, per
+ * residue row g of the packed inputs (protein b's node i at row prot_offsets[b] + i, i < n_b;
+ * rows n_b.. of a protein are zero / -1):
+ *   senders_out       [R, 50]     int32  neighbour node index within the protein, nearest first
+ *                                        (for n_b <= 50: all n_b nodes, self first; -1 after)
+ *   edge_features_out [R, 50, 27] f32    [rbf15, p3, q3, k3, t3]; for n_b <= 50 row-major over
+ *                                        the reference's n_b x n_b enumeration
+ *   ca_out            [R, 3]      f64    C-alpha coordinates (the graph's node_features)
+ *   n_nodes_out       [B]         int32  n_b
+ * Size gates as pst_tokenize. Invalidates pst_aux / pst_codebook_aux of an earlier call.
+ * Python: pst_amd.graph.build_protein_graphs pads these into the reference's ProteinGraph.
+ */
+int pst_build_graph(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags,
+                    const int64_t* prot_offsets, int32_t n_prot, int32_t* senders_out,
+                    float* edge_features_out, double* ca_out, int32_t* n_nodes_out);
+
+/*
  * Non-token QuantizerOutput fields of the LAST tokenize call, copied to host:
  *   bounded  [R, D]   continuous_embedding (tanh-bounded latents, masked)
  *   quantize [R, D]   quantize (rounded codes)

@@ -477,7 +477,7 @@ int validate(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot) {
 }
 
 int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t* offsets, int32_t n_prot,
-        uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes) {
+        uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes, bool graph_only = false) {
   const int64_t R = offsets[n_prot];
   int rc = ensure_workspace(ctx, R, n_prot);
   if (rc) return rc;
@@ -507,6 +507,12 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   pst::KnnArgs ka{Rpad, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, w.senders, w.deg, w.feat};
   pst::launch_knn(ka, st);
   mark(ctx, 2);
+  if (graph_only) {  // pst_build_graph: the encoder's outputs of an earlier call are gone
+    HIPCHK(hipGetLastError());
+    ctx->last_R = 0;
+    ctx->last_Rpad = Rpad;
+    return PST_OK;
+  }
 
   const float* A = ctx->d_arena;
   auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(A + o); };
@@ -801,6 +807,47 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
   if (n_nodes_out)
     HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  return PST_OK;
+}
+
+int pst_build_graph(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,
+                    int32_t n_prot, int32_t* senders_out, float* edge_features_out, double* ca_out,
+                    int32_t* n_nodes_out) {
+  if (!ctx) return PST_E_INVALID;
+  ctx->err.clear();
+  if (!atom_pos || !atom_flags || !senders_out || !edge_features_out || !ca_out || !n_nodes_out)
+    return fail(ctx, PST_E_INVALID, "null host buffer");
+  int rc = validate(ctx, offsets, n_prot);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t R = offsets[n_prot];
+  rc = ensure_workspace(ctx, R, n_prot);
+  if (rc) return rc;
+  auto& w = ctx->w;
+  HIPCHK(hipMemcpyAsync(w.pos, atom_pos, sizeof(double) * 111 * R, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(w.flags, atom_flags, 37 * R, hipMemcpyHostToDevice, ctx->stream));
+  rc = run(ctx, w.pos, w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes, /*graph_only=*/true);
+  if (rc) return rc;
+  std::vector<int32_t> snd((size_t)R * KNN);
+  std::vector<float> feat((size_t)R * KNN * 32);
+  HIPCHK(hipMemcpyAsync(snd.data(), w.senders, sizeof(int32_t) * snd.size(), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(feat.data(), w.feat, sizeof(float) * feat.size(), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ca_out, w.ca, sizeof(double) * 3 * R, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  // global residue slots → per-protein node indices; the 27 features of the 32-wide rows
+  for (int b = 0; b < n_prot; ++b) {
+    const int64_t base = offsets[b], end = offsets[b + 1];
+    for (int64_t g = base; g < end; ++g) {
+      const bool real = g - base < n_nodes_out[b];
+      for (int j = 0; j < KNN; ++j) {
+        const size_t e = (size_t)g * KNN + j;
+        senders_out[e] = real && snd[e] >= 0 ? (int32_t)(snd[e] - base) : -1;
+        for (int c = 0; c < 27; ++c) edge_features_out[e * 27 + c] = real ? feat[e * 32 + c] : 0.0f;
+      }
+      if (!real) ca_out[3 * g] = ca_out[3 * g + 1] = ca_out[3 * g + 2] = 0.0;
+    }
+  }
   return PST_OK;
 }
 

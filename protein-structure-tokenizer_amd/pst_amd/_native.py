@@ -39,7 +39,7 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_codebook_aux_device", "pst_pdb_parse_files", "pst_pdb_parse_strings",
            "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free",
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
-           "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_debug")
+           "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_debug", "pst_build_graph")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -76,6 +76,7 @@ def lib():
         L.pst_tokenize.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
         L.pst_tokenize_device.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
         L.pst_aux.argtypes = [P, P, P, P]
+        L.pst_build_graph.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P, P]
         L.pst_codebook_aux.argtypes = [P, P, P, P, P, P, ctypes.c_int64]
         L.pst_codebook_aux_device.argtypes = [P, P, P, P, P, ctypes.c_int64]
         L.pst_sync.argtypes = [P]
@@ -281,6 +282,22 @@ class Tokenizer:
 
     def sync(self):
         self._check(lib().pst_sync(self._h))
+
+    def build_graph_packed(self, pos, flags, offsets):
+        """Residue graphs of a packed batch (pst_build_graph): senders [R,50] int32 (node index
+        within the protein, -1 = none), edge features [R,50,27] f32, C-alpha [R,3] f64, n_nodes [B]."""
+        pos = np.ascontiguousarray(pos, np.float64)
+        flags = np.ascontiguousarray(flags, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        B = len(offsets) - 1
+        R = int(offsets[-1])
+        snd = np.zeros((max(R, 1), 50), np.int32)
+        feat = np.zeros((max(R, 1), 50, 27), np.float32)
+        ca = np.zeros((max(R, 1), 3), np.float64)
+        nn = np.zeros(B, np.int32)
+        self._check(lib().pst_build_graph(self._h, _ptr(pos), _ptr(flags), _ptr(offsets), B, _ptr(snd), _ptr(feat),
+                                          _ptr(ca), _ptr(nn)))
+        return snd, feat, ca, nn
 
     def aux(self, R: int):
         b = np.zeros((R, self.D), np.float32)

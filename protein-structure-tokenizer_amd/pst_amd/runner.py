@@ -5,8 +5,11 @@ into libpst (`include/pst.h`):
 
   reference (JAX / haiku, pmap over local devices)      here (libpst contexts, one per GPU)
   ----------------------------------------------------  -------------------------------------
-  make_graph_from_pdb  (:40-74)  parse + size gates +   parse + the same size gates; the graph
-                       preprocess_sample on the host    itself is built on the GPU (k_prep/k_knn)
+  make_graph_from_pdb  (:40-74)  parse + size gates +   parse + the same size gates; returns a
+                       preprocess_sample on the host    ProteinGraphView: the graph is built on the
+                                                        GPU (k_prep/k_knn) inside pst_tokenize, or
+                                                        padded like the reference's ProteinGraph
+                                                        on field access (pst_build_graph)
   batch_collate        (:77-83)  stack padded graphs    pack ragged atom37 arrays + offsets
   load_params          (:136-150) npz + pickled treedef npz + leaf order of full_param_spec
   params_keys_conversion (:153-165)                     same (pst_amd.params)
@@ -28,6 +31,7 @@ from typing import Any, Callable, Dict, List, NamedTuple, Optional, Sequence, Tu
 import numpy as np
 
 from . import _native
+from . import graph as _graph
 from . import params as _params
 from .config import LEVELS, TokenizerConfig
 from .sample import ProteinStructureSample
@@ -39,11 +43,13 @@ PARSE_THREADS = int(os.environ.get("PST_PARSE_THREADS", "8"))
 # ------------------------------------------------------------------------------- graph inputs
 def make_graph_from_pdb(pdb_file_path: str, num_neighbor: int, downsampling_ratio: int,
                         residue_loc_is_alphac: bool, padding_num_residue: int,
-                        sample: Optional[ProteinStructureSample] = None) -> ProteinStructureSample:
+                        sample: Optional[ProteinStructureSample] = None) -> _graph.ProteinGraphView:
     """Parse one PDB and apply the reference's size gates (`inference_runner.py:40-74`).
 
-    Returns the parsed structure; the residue graph (`preprocess_sample`) is built on the GPU
-    by `pst_tokenize`, so nothing else happens on the host. Parsing uses libpst's native
+    Returns a `ProteinGraphView`: the parsed structure, which `pst_tokenize` turns into the
+    residue graph on the GPU inside the tokenize call, and which also reads as the reference's
+    padded `ProteinGraph` (fields built by `pst_build_graph` on first access), so callers that
+    inspect the graph get the reference's arrays. Parsing uses libpst's native
     parser (`pst_pdb_parse_files`, Biopython semantics as restated in `pst_amd/pdb.py`);
     `sample` skips parsing when the caller parsed a batch already. `residue_loc_is_alphac=False`
     and other `padding_num_residue` / `num_neighbor` values than the shipped 512 / 50 are
@@ -71,7 +77,7 @@ def make_graph_from_pdb(pdb_file_path: str, num_neighbor: int, downsampling_rati
         raise NotImplementedError("libpst is specialised for graph_max_neighbor=50, seq_max_size=512")
     if downsampling_ratio not in (1, 2, 4):
         raise ValueError(f"downsampling_ratio must be 1, 2 or 4, got {downsampling_ratio}")
-    return sample
+    return _graph.ProteinGraphView(sample, downsampling_ratio)
 
 
 class ProteinBatch(NamedTuple):
@@ -89,7 +95,15 @@ def batch_collate(batch_dims: List[int], batch_of_samples: List[ProteinStructure
     """Mirror of `inference_runner.py:77-83` (same count check as the reshape there)."""
     if int(np.prod(batch_dims)) != len(batch_of_samples):
         raise ValueError(f"cannot reshape {len(batch_of_samples)} samples into {list(batch_dims)}")
-    return ProteinBatch(tuple(int(b) for b in batch_dims), tuple(batch_of_samples))
+    samples = []
+    for s in batch_of_samples:
+        if isinstance(s, _graph.ProteinGraphView):
+            s = s.sample
+        if not isinstance(s, ProteinStructureSample):
+            raise TypeError("batch_collate takes the structures make_graph_from_pdb returns "
+                            f"(the GPU builds the graph from atom37 arrays), got {type(s).__name__}")
+        samples.append(s)
+    return ProteinBatch(tuple(int(b) for b in batch_dims), tuple(samples))
 
 
 # ------------------------------------------------------------------------------------ params

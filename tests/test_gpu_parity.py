@@ -250,3 +250,37 @@ def test_fused_and_split_layers_identical(split, monkeypatch):
     s = samples[2]
     o = O.tokenize(blob, LEVELS[4096], 1, s.atom37_positions, s.atom_flags())
     assert np.array_equal(tok[off[2]: off[2] + nt[2]], o["tokens"])
+
+
+def test_build_graph_matches_reference_padded_graphs():
+    """pst_build_graph + the host padding == the reference's preprocess_sample(...).graph for
+    every graph_golden case, in one ragged batch (edge features bitwise as float32)."""
+    from test_graph_host import CASES, PG, check_graph
+    from pst_amd import graph as Gr
+    G = np.load(os.path.join(GOLD, "graph_golden.npz"))
+    by_df = {}
+    for c in CASES:
+        by_df.setdefault(int(G[c + "/df"]), []).append(c)
+    tk = tokenizer(4096, 1)
+    for df, cases in by_df.items():
+        graphs = Gr.build_protein_graphs(tk, [_samples_from(G, c) for c in cases], df)
+        for c, g in zip(cases, graphs):
+            check_graph(g, c)
+    # the tokenize path still works on the same context afterwards
+    s = synthetic.synthetic_protein(64, 9)
+    assert np.array_equal(tk.tokenize([s])[0], O.tokenize(P.random_blob(6, 1234), LEVELS[4096], 1, s.atom37_positions, s.atom_flags())["tokens"])
+
+
+def test_make_graph_from_pdb_reads_as_reference_graph(tmp_path):
+    """runner.make_graph_from_pdb on CASP14 T1024: the returned view's ProteinGraph fields equal
+    the reference's graph of the same file."""
+    import tarfile
+    from test_graph_host import check_graph
+    from pst_amd import runner
+    with tarfile.open(os.path.join(GOLD, "casp14_pdbs.tar.gz")) as tf:
+        m = [x for x in tf.getmembers() if x.name.endswith("T1024.pdb")][0]
+        tf.extract(m, tmp_path)
+    v = runner.make_graph_from_pdb(str(tmp_path / m.name), num_neighbor=50, downsampling_ratio=1,
+                                   residue_loc_is_alphac=True, padding_num_residue=512)
+    check_graph(v.graph, "casp_T1024_df1")
+    assert np.array_equal(v.senders, v.graph.senders) and v.nb_residues == 391
