@@ -730,9 +730,9 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 
 // Split layer (small batches, where one wave per 32 receivers cannot fill the GPU): the edge
 // blocks of all tasks run in parallel, `blocks_per_wave` consecutive blocks per wave, and store
-// their messages as rows `msg_rows[E][128]` (perm order); k_mpnn_node then forms each receiver's
+// their messages as rows `msg_rows[E][128]` (perm order); k_seg_sum forms each receiver's
 // ordered segment sum from those rows — the same additions in the same order as k_mpnn, so
-// both modes give identical bits.
+// both modes give identical bits — and k_mpnn_node runs the node update on the sums.
 __device__ __forceinline__ int64_t gb_edge(int64_t gb, int lane) { return gb * 32 + (lane & 31); }
 
 template <int LAYER>
@@ -756,6 +756,27 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_edge(MpnnArgs a) 
   }
 }
 
+// Ordered segment sums of the split schedule, one wave per receiver: lane l sums channels
+// (2l, 2l+1) of the perm-ordered message rows over the receiver's slots in order,
+// agg = ((0 + m_0) + m_1) + ... + m_{deg-1} — the fused kernel's additions in its order. Reads
+// are whole 512-byte rows per step; thousands of waves keep HBM busy where the 32-receiver node
+// tiles alone could not.
+__global__ __launch_bounds__(256) void k_seg_sum(const float* __restrict__ msg_rows, const int32_t* __restrict__ deg,
+                                                 float* __restrict__ agg, int64_t n_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= n_rows) return;
+  const int d = deg[g];
+  const float2* row = reinterpret_cast<const float2*>(msg_rows + g * KNN * 128) + lane;
+  float2 acc = make_float2(0.0f, 0.0f);
+  for (int j = 0; j < d; ++j) {
+    const float2 v = row[j * 64];
+    acc.x = acc.x + v.x;
+    acc.y = acc.y + v.y;
+  }
+  reinterpret_cast<float2*>(agg + g * 128)[lane] = acc;
+}
+
 template <int LAYER>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_node(MpnnArgs a) {
   const int lane = threadIdx.x & 63;
@@ -763,30 +784,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_node(MpnnArgs a) 
   const int64_t task = (int64_t)blockIdx.x * 4 + w;
   if (task >= a.n_tasks) return;
   const int64_t g0 = task * 32;
-  const int64_t gl = g0 + (lane & 31);
-  const int deg = a.deg[gl];
-  // agg = ((0 + m_0) + m_1) + ... + m_{deg-1}, per channel (this lane's 64 channels); each lane
-  // stores and re-reads only its own half row, so no barrier is needed
-  float* aggl = a.agg + task * 32 * 128;
-  {
-    Tile ag;
-    tile_zero(ag);
-    const float4* row = reinterpret_cast<const float4*>(a.msg_rows + gl * KNN * 128 + (lane >> 5) * 64);
-    for (int j = 0; j < deg; ++j) {
-#pragma unroll
-      for (int M = 0; M < 4; ++M)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = row[j * 32 + M * 4 + q];
-          ag.m[M][4 * q + 0] = ag.m[M][4 * q + 0] + v.x;
-          ag.m[M][4 * q + 1] = ag.m[M][4 * q + 1] + v.y;
-          ag.m[M][4 * q + 2] = ag.m[M][4 * q + 2] + v.z;
-          ag.m[M][4 * q + 3] = ag.m[M][4 * q + 3] + v.w;
-        }
-    }
-    tile_store_perm(ag, aggl + (lane & 31) * 128);
-  }
-  node_update<LAYER>(a, lane, g0, aggl);
+  node_update<LAYER>(a, lane, g0, a.agg + task * 32 * 128);  // sums from k_seg_sum
 }
 
 // ---------------------------------------------------------------------------- k_down
@@ -1028,6 +1026,8 @@ void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st) {
     if (layer == 0) hipLaunchKernelGGL(k_mpnn_edge<0>, egrid, dim3(256), 0, st, a);
     else if (layer == 1) hipLaunchKernelGGL(k_mpnn_edge<1>, egrid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_mpnn_edge<2>, egrid, dim3(256), 0, st, a);
+    const int64_t rows = a.n_tasks * 32;
+    hipLaunchKernelGGL(k_seg_sum, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a.msg_rows, a.deg, a.agg, rows);
     if (layer == 0) hipLaunchKernelGGL(k_mpnn_node<0>, grid, dim3(256), 0, st, a);
     else if (layer == 1) hipLaunchKernelGGL(k_mpnn_node<1>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_mpnn_node<2>, grid, dim3(256), 0, st, a);
