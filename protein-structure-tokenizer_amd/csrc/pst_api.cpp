@@ -19,8 +19,18 @@ namespace {
 
 constexpr int H = 128;
 constexpr int KNN = 50;
-// split MPNN mode up to this many 32-receiver tasks (PST_SPLIT_TASKS overrides; measured in DESIGN.md)
-constexpr int64_t PST_SPLIT_TASKS_DEFAULT = 1024;
+// MPNN schedule choice (measured on MI355X with tools/split_ab.sh). The fused
+// kernel runs one wave per 32-receiver task at 2 waves/SIMD, so its time steps with
+// k = ceil(tasks / SIMDs): about k·SIMDs task-units for k >= 2 and 1.1·SIMDs for k = 1 (one
+// wave per SIMD runs alone). The split schedule costs about 1.1 units per task (message rows
+// through HBM). Split wins below ~1 000 tasks and in the half-empty rounds above.
+constexpr double SPLIT_COST_PER_TASK = 1.1;
+constexpr double FUSED_SINGLE_ROUND = 1.1;
+bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
+  const int64_t k = (n_tasks + n_simds - 1) / n_simds;
+  const double fused = k <= 1 ? FUSED_SINGLE_ROUND * (double)n_simds : (double)(k * n_simds);
+  return SPLIT_COST_PER_TASK * (double)n_tasks < fused;
+}
 
 thread_local std::string g_create_error;
 
@@ -222,7 +232,8 @@ struct pst_ctx {
   // grow-only per-edge message rows of the split MPNN mode (small batches only)
   float* msg = nullptr;
   size_t msg_bytes = 0;
-  int64_t split_tasks = -1;  // split mode when n_tasks <= this (PST_SPLIT_TASKS; <0 = unset)
+  int64_t split_tasks = -2;  // PST_SPLIT_TASKS: split iff n_tasks <= this; -1 = cost model; -2 = not read yet
+  int64_t n_simds = 1024;    // 4 x compute units of the device
   std::vector<int64_t> h_offsets;
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
@@ -519,16 +530,18 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   auto mlp = [&](const MlpOff& o) {
     return pst::MlpW{F4(o.w0), A + o.b0, F4(o.w1), A + o.b1, F4(o.w2), A + o.b2, F4(o.bf1), F4(o.bf2)};
   };
-  // Small batches (n_tasks waves cannot fill 256 CUs x 8 wave slots) run each layer split in two
-  // launches, edge blocks spread over ~4096 waves, messages through HBM; bit-identical results.
+  // Batches whose 32-receiver tasks leave fused rounds half empty (use_split_schedule) run each
+  // layer split: edge blocks spread over ~4096 waves, messages through HBM, ordered sums in
+  // k_seg_sum, node update; bit-identical results.
   const int64_t n_tasks = Rpad / 32;
-  if (ctx->split_tasks < 0) {
+  if (ctx->split_tasks == -2) {
     const char* e = getenv("PST_SPLIT_TASKS");
-    ctx->split_tasks = e ? std::max<int64_t>(0, atoll(e)) : PST_SPLIT_TASKS_DEFAULT;
+    ctx->split_tasks = e ? std::max<int64_t>(0, atoll(e)) : -1;
   }
+  const bool split = ctx->split_tasks >= 0 ? n_tasks <= ctx->split_tasks : use_split_schedule(n_tasks, ctx->n_simds);
   float* msg_rows = nullptr;
   int32_t bpw = 1;
-  if (n_tasks <= ctx->split_tasks) {
+  if (split) {
     const size_t need = (size_t)n_tasks * 32 * KNN * 128 * sizeof(float);
     if (need > ctx->msg_bytes) {
       if (ctx->msg) (void)hipFree(ctx->msg);
@@ -730,6 +743,12 @@ int pst_create(int32_t device, const pst_model_desc* desc, const float* params, 
     delete ctx;
     return PST_E_HIP;
   }
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      ctx->n_simds = 4 * (int64_t)prop.multiProcessorCount;
+  }
+
   int rc = build_weights(ctx, params);
   if (rc) {
     g_create_error = ctx->err;
