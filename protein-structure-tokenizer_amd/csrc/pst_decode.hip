@@ -23,6 +23,8 @@
 
 #include "../../include/pst.h"
 #include "pst_backbone_tables.h"
+#include "pst_device.h"
+#include "pst_frag.h"
 #include "pst_pe.h"
 
 namespace pst {
@@ -269,6 +271,138 @@ __global__ void k_pair_product(const float* __restrict__ left, const float* __re
   const int64_t i = n0 + loc / Nb, j = n0 + loc % Nb;
   const int c = threadIdx.x;
   P[pr * 256 + c] = left[i * 256 + c] * right[j * 256 + c];
+}
+
+// ---------------------------------------------------------------- fused pair representation
+// The whole per-pair chain of the sequence decoder and the structure module's pair inputs in one
+// pass over 32-pair wave tiles (pst_device.h layout, f32 MFMA), instead of ~12 library GEMMs and
+// elementwise passes over N² × 256 tensors in HBM (sequence_decoder.py:69-99, folding.py:260-275):
+//   P      = left[i] ⊙ right[j]                                  (256)
+//   pair0  = LN_out( out2(relu(out1(P))) + right1(P) )           (128)
+//   lin    = seq_linear([PE(j − i) | pair0]) = U[j − i] + pair0 · W_seq[128:256]
+//            (U = PE · W_seq[0:128] + b, a 1 023-row table built at pst_decoder_create)
+//   z      = pt2(relu(pt1(LN_pt(lin))))                          (Transition output, 128)
+//   zln    = LN_pair(z);  b2d = (zln · W_att2d + b) / sqrt(3)     (12 heads)
+// Only zln and b2d go to HBM (z too when the decoder keeps debug intermediates).
+struct PairArgs {
+  const float* left;   // [N][256] natural
+  const float* right;  // [N][256]
+  const float4* f_out1[2][2];  // [k chunk][out chunk]
+  const float* pb_out1[2];     // perm bias chunks (applied with the ReLU, just in time)
+  const float4* f_out2[2];
+  const float4* bf_out2;
+  const float4* f_r1[2];
+  const float* pb_r1;
+  const float *ln1_s, *ln1_o;  // pair representation out LN (perm)
+  const float* U;              // [1023][128] perm
+  const float4* f_seqb;
+  const float *ln2_s, *ln2_o;  // transition input LN
+  const float4* f_pt1[2];
+  const float* pb_pt1[2];
+  const float4* f_pt2[2];
+  const float4* bf_pt2;
+  const float *ln3_s, *ln3_o;  // structure-module pair LN
+  const float* f_att2d;        // narrow fragments [64][64]
+  const float* b_att2d;        // [12]
+  float* z;                    // [NP][128] natural, or null
+  float* zln;                  // [NP][128] natural
+  float* b2d;                  // [NP][12]
+  int64_t NP;
+  DecBatch bt;
+};
+
+// natural-order 128-channel rows <-> the wave tile (lane half h holds channels 32M + 8q + 4h + i)
+__device__ __forceinline__ void tile_load_nat(Tile& t, const float* __restrict__ row) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(row + 32 * M + 8 * q + 4 * h);
+      t.m[M][4 * q + 0] = v.x;
+      t.m[M][4 * q + 1] = v.y;
+      t.m[M][4 * q + 2] = v.z;
+      t.m[M][4 * q + 3] = v.w;
+    }
+}
+__device__ __forceinline__ void tile_store_nat(const Tile& t, float* __restrict__ row) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(row + 32 * M + 8 * q + 4 * h) =
+          make_float4(t.m[M][4 * q], t.m[M][4 * q + 1], t.m[M][4 * q + 2], t.m[M][4 * q + 3]);
+}
+__device__ __forceinline__ void tile_mul_nat(Tile& t, const float* __restrict__ row) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(row + 32 * M + 8 * q + 4 * h);
+      t.m[M][4 * q + 0] *= v.x;
+      t.m[M][4 * q + 1] *= v.y;
+      t.m[M][4 * q + 2] *= v.z;
+      t.m[M][4 * q + 3] *= v.w;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pair_fused(PairArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + (lane & 31);
+  if (((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 >= a.NP) return;  // wave-uniform
+  const bool valid = p < a.NP;
+  const int64_t pc = valid ? p : a.NP - 1;
+  const int b = pair_protein(a.bt, pc);
+  const int64_t n0 = a.bt.node_off[b];
+  const int64_t Nb = a.bt.node_off[b + 1] - n0, loc = pc - a.bt.pair_off[b];
+  const int64_t il = loc / Nb, jl = loc - il * Nb;
+  const float* lrow = a.left + (n0 + il) * 256;
+  const float* rrow = a.right + (n0 + jl) * 256;
+  Tile A0, A1, H, Q;
+  tile_load_nat(A0, lrow);
+  tile_mul_nat(A0, rrow);
+  tile_load_nat(A1, lrow + 128);
+  tile_mul_nat(A1, rrow + 128);
+  // pair0 = out2(relu(out1(P) + b1)) + b2 + right1(P) + b_r1, then LN
+  tile_zero(H);
+  tile_gemm(H, A0, a.f_out1[0][0]);
+  tile_gemm(H, A1, a.f_out1[1][0]);
+  tile_gemm_bf(Q, H, a.f_out2[0], a.bf_out2, ActBiasRelu{a.pb_out1[0]});
+  tile_zero(H);
+  tile_gemm(H, A0, a.f_out1[0][1]);
+  tile_gemm(H, A1, a.f_out1[1][1]);
+  tile_gemm_f(Q, H, a.f_out2[1], ActBiasRelu{a.pb_out1[1]});
+  tile_gemm(Q, A0, a.f_r1[0]);
+  tile_gemm(Q, A1, a.f_r1[1]);
+  tile_add_vec(Q, a.pb_r1);
+  tile_layer_norm(Q, a.ln1_s, a.ln1_o);
+  // seq_linear over [PE(j - i) | pair0]
+  tile_load_perm(A0, a.U + (jl - il + 511) * 128);
+  tile_gemm(A0, Q, a.f_seqb);
+  tile_layer_norm(A0, a.ln2_s, a.ln2_o);
+  // transition (no residual): z = pt2(relu(pt1(x) + b1)) + b2
+  tile_zero(H);
+  tile_gemm(H, A0, a.f_pt1[0]);
+  tile_gemm_bf(Q, H, a.f_pt2[0], a.bf_pt2, ActBiasRelu{a.pb_pt1[0]});
+  tile_zero(H);
+  tile_gemm(H, A0, a.f_pt1[1]);
+  tile_gemm_f(Q, H, a.f_pt2[1], ActBiasRelu{a.pb_pt1[1]});
+  if (a.z && valid) tile_store_nat(Q, a.z + p * 128);
+  tile_layer_norm(Q, a.ln3_s, a.ln3_o);
+  if (valid) tile_store_nat(Q, a.zln + p * 128);
+  // attention 2-D bias: 12 outputs of one narrow accumulator (rows = output channels)
+  f32x16 acc = {};
+  tile_gemm_narrow(acc, Q, a.f_att2d);
+  if (valid) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (o < 12) a.b2d[p * 12 + o] = (acc[r] + a.b_att2d[o]) * 0.577350269189626f;
+    }
+  }
 }
 
 // C[pair (i, j)] = [PE(j - i; 512) | pair0[pair]] (sequence_decoder.py:69-99)
@@ -582,8 +716,10 @@ struct pst_decoder {
   float* d_pe_tok = nullptr;   // PE(t; 512/df) [512/df][128]
   float* d_pe_rel = nullptr;   // PE(d; 512), d = -511..511 [1023][128]
   float* d_pw = nullptr;       // IPA point weights [12]
-  rocblas_handle blas = nullptr;  // the large pair-representation GEMMs (plain library GEMMs)
+  rocblas_handle blas = nullptr;  // library GEMMs (per-node rows; pair rows only when unfused)
   DecWeights W{};
+  float* d_pair = nullptr;  // fused pair kernel: fragments, perm vectors, U table (k_pair_fused)
+  PairArgs pair{};          // pointers into d_pair (per-call fields filled by decode_group)
   // scratch (grow-only, sized for N = 512)
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -849,24 +985,40 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.pr_ln_in);
   gemm(st, S.ln_a, 128, W.left, S.left, 256, Ni, 0);
   gemm(st, S.ln_a, 128, W.right, S.right, 256, Ni, 0);
-  hipLaunchKernelGGL(k_pair_product, dim3((unsigned)NP), dim3(256), 0, st, S.left, S.right, S.P, bt);
-  gemm(st, S.P, 256, W.out1, S.h1, 256, NPi, F_RELU_OUT);
-  gemm(st, S.h1, 256, W.out2, S.pair0, 128, NPi, 0);
-  gemm(st, S.P, 256, W.right1, S.lin_out, 128, NPi, 0);
-  hipLaunchKernelGGL(k_add, dim3((unsigned)((NP * 128 + 255) / 256)), dim3(256), 0, st, S.pair0, S.lin_out, NP * 128);
-  layernorm(st, S.pair0, 128, S.pair0, 128, NPi, 128, W.pr_ln_out);
-  hipLaunchKernelGGL(k_pair_concat, dim3((unsigned)NP), dim3(128), 0, st, dec->d_pe_rel, S.pair0, S.catb, bt);
-  gemm(st, S.catb, 256, W.seq_linear, S.lin_out, 128, NPi, 0);
-  layernorm(st, S.lin_out, 128, S.lnz, 128, NPi, 128, W.pt_ln);
-  gemm(st, S.lnz, 128, W.pt1, S.h1, 256, NPi, F_RELU_OUT);
-  gemm(st, S.h1, 256, W.pt2, S.z, 128, NPi, 0);  // z_ij (Transition output, no residual)
-  // ---- structure module
-  layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
-  gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
-  layernorm(st, S.z, 128, S.zln, 128, NPi, 128, W.pair_ln);
-  gemm(st, S.zln, 128, W.att2d, S.b2d, 12, NPi, 0);
-  hipLaunchKernelGGL(k_scale, dim3((unsigned)((NP * 12 + 255) / 256)), dim3(256), 0, st, S.b2d, NP * 12,
-                     0.577350269189626f);
+  const bool fused = !getenv("PST_DECODE_UNFUSED");
+  if (fused) {
+    layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
+    gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
+    PairArgs pa = dec->pair;
+    pa.left = S.left;
+    pa.right = S.right;
+    pa.z = keep_debug ? S.z : nullptr;
+    pa.zln = S.zln;
+    pa.b2d = S.b2d;
+    pa.NP = NP;
+    pa.bt = bt;
+    const int64_t tiles = (NP + 31) / 32;
+    hipLaunchKernelGGL(k_pair_fused, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, pa);
+  } else {
+    hipLaunchKernelGGL(k_pair_product, dim3((unsigned)NP), dim3(256), 0, st, S.left, S.right, S.P, bt);
+    gemm(st, S.P, 256, W.out1, S.h1, 256, NPi, F_RELU_OUT);
+    gemm(st, S.h1, 256, W.out2, S.pair0, 128, NPi, 0);
+    gemm(st, S.P, 256, W.right1, S.lin_out, 128, NPi, 0);
+    hipLaunchKernelGGL(k_add, dim3((unsigned)((NP * 128 + 255) / 256)), dim3(256), 0, st, S.pair0, S.lin_out, NP * 128);
+    layernorm(st, S.pair0, 128, S.pair0, 128, NPi, 128, W.pr_ln_out);
+    hipLaunchKernelGGL(k_pair_concat, dim3((unsigned)NP), dim3(128), 0, st, dec->d_pe_rel, S.pair0, S.catb, bt);
+    gemm(st, S.catb, 256, W.seq_linear, S.lin_out, 128, NPi, 0);
+    layernorm(st, S.lin_out, 128, S.lnz, 128, NPi, 128, W.pt_ln);
+    gemm(st, S.lnz, 128, W.pt1, S.h1, 256, NPi, F_RELU_OUT);
+    gemm(st, S.h1, 256, W.pt2, S.z, 128, NPi, 0);  // z_ij (Transition output, no residual)
+    // ---- structure module
+    layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
+    gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
+    layernorm(st, S.z, 128, S.zln, 128, NPi, 128, W.pair_ln);
+    gemm(st, S.zln, 128, W.att2d, S.b2d, 12, NPi, 0);
+    hipLaunchKernelGGL(k_scale, dim3((unsigned)((NP * 12 + 255) / 256)), dim3(256), 0, st, S.b2d, NP * 12,
+                       0.577350269189626f);
+  }
   hipLaunchKernelGGL(k_affine_init, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, Ni);
   for (int it = 0; it < 8; ++it) {
     gemm(st, S.act, 384, W.q_scalar, S.qs, 192, Ni, 0);
@@ -942,6 +1094,77 @@ size_t pst_decoder_param_count(int32_t n_levels) {
 
 const char* pst_decoder_create_error(void) { return g_dec_create_error.c_str(); }
 
+namespace {
+// Pack the pair-chain weights for k_pair_fused (host weights Wh from walk_decoder on the blob).
+int build_pair_arena(pst_decoder* dec, const DecWeights& Wh) {
+  using namespace pst_host;
+  const int H = 128;
+  std::vector<float> A;
+  auto add = [&](const std::vector<float>& v) {
+    const size_t o = A.size();
+    A.insert(A.end(), v.begin(), v.end());
+    A.resize((A.size() + 63) / 64 * 64, 0.0f);
+    return o;
+  };
+  size_t f_out1[2][2], f_out2[2], f_r1[2], f_pt1[2], f_pt2[2], pb_out1[2], pb_pt1[2];
+  for (int kc = 0; kc < 2; ++kc)
+    for (int oc = 0; oc < 2; ++oc) f_out1[kc][oc] = add(frag(Wh.out1.w, 2 * H, H * kc, H, H, H * oc, H));
+  for (int kc = 0; kc < 2; ++kc) {
+    f_out2[kc] = add(frag(Wh.out2.w, H, H * kc, H, H, 0, H));
+    f_r1[kc] = add(frag(Wh.right1.w, H, H * kc, H, H, 0, H));
+    f_pt2[kc] = add(frag(Wh.pt2.w, H, H * kc, H, H, 0, H));
+    f_pt1[kc] = add(frag(Wh.pt1.w, 2 * H, 0, H, H, H * kc, H));
+    pb_out1[kc] = add(perm(Wh.out1.b + H * kc));
+    pb_pt1[kc] = add(perm(Wh.pt1.b + H * kc));
+  }
+  const size_t bf_out2 = add(bfrag(Wh.out2.b)), bf_pt2 = add(bfrag(Wh.pt2.b)), pb_r1 = add(perm(Wh.right1.b));
+  const size_t f_seqb = add(frag(Wh.seq_linear.w, H, H, H, H, 0, H));
+  const size_t ln1s = add(perm(Wh.pr_ln_out.s)), ln1o = add(perm(Wh.pr_ln_out.o));
+  const size_t ln2s = add(perm(Wh.pt_ln.s)), ln2o = add(perm(Wh.pt_ln.o));
+  const size_t ln3s = add(perm(Wh.pair_ln.s)), ln3o = add(perm(Wh.pair_ln.o));
+  const size_t f_att = add(frag_narrow(Wh.att2d.w, 12, 12));
+  const size_t b_att = add(std::vector<float>(Wh.att2d.b, Wh.att2d.b + 12));
+  // U[d] = PE(d - 511; 512) · W_seq[0:128] + b_seq (float64 accumulation, rounded once)
+  std::vector<float> pe = pst::pe_rows(-511, 1023, 512), U((size_t)1023 * H);
+  for (int d = 0; d < 1023; ++d)
+    for (int o = 0; o < H; ++o) {
+      double acc = Wh.seq_linear.b[o];
+      for (int c = 0; c < H; ++c) acc += (double)pe[(size_t)d * H + c] * (double)Wh.seq_linear.w[(size_t)c * H + o];
+      U[(size_t)d * H + o] = (float)acc;
+    }
+  const size_t u_tab = add(perm_rows(U, 1023));
+  if (hipMalloc(&dec->d_pair, A.size() * sizeof(float)) != hipSuccess ||
+      hipMemcpy(dec->d_pair, A.data(), A.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+    return 1;
+  const float* D = dec->d_pair;
+  auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(D + o); };
+  PairArgs& P = dec->pair;
+  for (int kc = 0; kc < 2; ++kc) {
+    for (int oc = 0; oc < 2; ++oc) P.f_out1[kc][oc] = F4(f_out1[kc][oc]);
+    P.f_out2[kc] = F4(f_out2[kc]);
+    P.f_r1[kc] = F4(f_r1[kc]);
+    P.f_pt1[kc] = F4(f_pt1[kc]);
+    P.f_pt2[kc] = F4(f_pt2[kc]);
+    P.pb_out1[kc] = D + pb_out1[kc];
+    P.pb_pt1[kc] = D + pb_pt1[kc];
+  }
+  P.bf_out2 = F4(bf_out2);
+  P.bf_pt2 = F4(bf_pt2);
+  P.pb_r1 = D + pb_r1;
+  P.f_seqb = F4(f_seqb);
+  P.ln1_s = D + ln1s;
+  P.ln1_o = D + ln1o;
+  P.ln2_s = D + ln2s;
+  P.ln2_o = D + ln2o;
+  P.ln3_s = D + ln3s;
+  P.ln3_o = D + ln3o;
+  P.f_att2d = D + f_att;
+  P.b_att2d = D + b_att;
+  P.U = D + u_tab;
+  return 0;
+}
+}  // namespace
+
 int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* params, size_t n_params,
                        pst_decoder** out) {
   g_dec_create_error.clear();
@@ -1007,6 +1230,7 @@ int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* 
       pw[h] = base * sp;
     }
     if (!up(&dec->d_pw, pw)) return bad("point weight upload failed");
+    if (build_pair_arena(dec, Wh)) return bad("pair fragment upload failed");
   }
   *out = dec;
   return PST_OK;
@@ -1017,7 +1241,7 @@ int pst_decoder_destroy(pst_decoder* dec) {
   (void)hipSetDevice(dec->device);
   if (dec->stream) (void)hipStreamSynchronize(dec->stream);
   for (void* p : {(void*)dec->d_blob, (void*)dec->d_levels, (void*)dec->d_pe_node, (void*)dec->d_pe_tok,
-                  (void*)dec->d_pe_rel, (void*)dec->d_pw, dec->ws})
+                  (void*)dec->d_pe_rel, (void*)dec->d_pw, (void*)dec->d_pair, dec->ws})
     if (p) (void)hipFree(p);
   if (dec->blas) (void)rocblas_destroy_handle(dec->blas);
   if (dec->stream) (void)hipStreamDestroy(dec->stream);
