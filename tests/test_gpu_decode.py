@@ -107,3 +107,24 @@ def test_grouped_decode_matches_single():
         alone = dec.decode([want_tok])[0]
         assert np.max(np.abs(t - alone)) < 1e-3
     dec.close()
+
+
+def test_fused_pair_kernel_matches_library_path(monkeypatch):
+    """k_pair_fused (one kernel over 32-pair tiles) against the library-GEMM pair path
+    (PST_DECODE_UNFUSED=1) on the same tokens: pair representation and atoms agree to float32
+    reordering noise, for a group of several proteins of different lengths."""
+    monkeypatch.setenv("PST_DEBUG", "1")
+    from pst_amd._native import Decoder
+    rng = np.random.default_rng(5)
+    toks = [rng.integers(0, 4096, n) for n in (37, 96, 5)]
+    dec = Decoder(0, 4096, 1, P.pack_decoder(P.random_full_params(6, 9), 6))
+    n_pairs = sum(len(t) ** 2 for t in toks)
+    fused = dec.decode(toks)
+    z_fused = dec.debug(1, n_pairs * 128).copy()
+    monkeypatch.setenv("PST_DECODE_UNFUSED", "1")
+    ref = dec.decode(toks)
+    z_ref = dec.debug(1, n_pairs * 128)
+    dec.close()
+    assert np.max(np.abs(z_fused - z_ref)) / np.max(np.abs(z_ref)) < 2e-5
+    for a, b in zip(fused, ref):
+        assert np.max(np.abs(a - b)) < 1e-3
