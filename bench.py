@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_k_mpnn1.json"),
                     help="PMC-measured HBM bytes per residue of k_mpnn<1> (tools/pmc_traffic.sh)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, the driver's runs) or gloo (rehearsing several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -95,10 +97,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())
+    gpu = local % ndev  # one GPU per rank on a full node; ranks share GPUs only when rehearsing with gloo
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", gpu)
+    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     # synthetic workload of this rank (different proteins per rank)
     samples = synthetic.synthetic_batch(args.proteins, args.residues, seed=1000 + rank * 100_000)
@@ -112,7 +120,7 @@ def main():
     from pst_amd.config import LEVELS
     levels = LEVELS[args.codebook]
     blob = P.random_blob(len(levels), 1234)
-    tk = Tokenizer(local, args.codebook, args.df, blob)
+    tk = Tokenizer(gpu, args.codebook, args.df, blob)
     torch.cuda.synchronize(dev)
 
     def step():
@@ -134,7 +142,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     residues_per_rank = R
