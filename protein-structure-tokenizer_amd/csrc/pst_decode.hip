@@ -514,22 +514,48 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   const float* b2d = b2d_all + (bt.pair_off[bprot] + (int64_t)il * N) * 12;
   const float* zln = zln_all + (bt.pair_off[bprot] + (int64_t)il * N) * 128;
   const float sw = 0.144337567297406f;  // sqrt(1 / (3 * 16))
-  // logits
-  for (int e = tid; e < 12 * N; e += 256) {
-    const int h = e / N, j = e - h * N;
-    float sc = 0.0f;
-    const float* q = qs + ig * 192 + h * 16;
-    const float* k = kvs + (int64_t)j * 384 + h * 32;
-    for (int c = 0; c < 16; ++c) sc = __builtin_fmaf(sw * q[c], k[c], sc);
-    float pt = 0.0f;
-    for (int p = 0; p < 4; ++p) {
-      const float* qp = qpg + ((ig * 12 + h) * 4 + p) * 3;
-      const float* kp = kvpg + (((int64_t)j * 12 + h) * 12 + p) * 3;
-      const float dx = qp[0] - kp[0], dy = qp[1] - kp[1], dz = qp[2] - kp[2];
-      const float d2 = (dx * dx + dy * dy) + dz * dz;
-      pt += pw[h] * d2;
+  // logits: one key per thread, all 12 heads, from 16-byte loads of the key's rows; the query
+  // (scaled scalar part and global points) is shared through LDS
+  __shared__ float qsh[192 + 144];
+  for (int e = tid; e < 192; e += 256) qsh[e] = sw * qs[ig * 192 + e];
+  for (int e = tid; e < 144; e += 256) qsh[192 + e] = qpg[ig * 144 + e];
+  __syncthreads();
+  for (int j = tid; j < N; j += 256) {
+    const float4* krow = reinterpret_cast<const float4*>(kvs + (int64_t)j * 384);
+    const float4* kprow = reinterpret_cast<const float4*>(kvpg + (int64_t)j * 432);
+    const float4* brow = reinterpret_cast<const float4*>(b2d + (int64_t)j * 12);
+    float bb[12];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const float4 v = brow[u];
+      bb[4 * u] = v.x; bb[4 * u + 1] = v.y; bb[4 * u + 2] = v.z; bb[4 * u + 3] = v.w;
     }
-    att[h][j] = (sc + (-0.5f * pt)) + b2d[(int64_t)j * 12 + h];
+#pragma unroll 2
+    for (int h = 0; h < 12; ++h) {
+      float k[16], kp[12];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = krow[h * 8 + u];
+        k[4 * u] = v.x; k[4 * u + 1] = v.y; k[4 * u + 2] = v.z; k[4 * u + 3] = v.w;
+      }
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const float4 v = kprow[h * 9 + u];
+        kp[4 * u] = v.x; kp[4 * u + 1] = v.y; kp[4 * u + 2] = v.z; kp[4 * u + 3] = v.w;
+      }
+      float sc = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) sc = __builtin_fmaf(qsh[h * 16 + c], k[c], sc);
+      float pt = 0.0f;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float* qp = qsh + 192 + (h * 4 + p) * 3;
+        const float dx = qp[0] - kp[3 * p], dy = qp[1] - kp[3 * p + 1], dz = qp[2] - kp[3 * p + 2];
+        const float d2 = (dx * dx + dy * dy) + dz * dz;
+        pt += pw[h] * d2;
+      }
+      att[h][j] = (sc + (-0.5f * pt)) + bb[h];
+    }
   }
   __syncthreads();
   // softmax per head (waves 0..3 take heads h, h+4, h+8)
