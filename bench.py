@@ -39,8 +39,10 @@ H, K = 128, 50
 MLP_FLOP = 2 * (3 * H * H + H * H + H * H)          # 163 840 per edge per 384-128-128-128 MLP
 MPNN1_ALG_FLOP_PER_RES = K * 2 * MLP_FLOP + 2 * (H * 4 * H + 4 * H * H)   # 16 646 144
 PATH_ALG_FLOP_PER_RES = {1: 44_715_008, 4: 44_395_904}  # SURVEY §8d, whole path per residue
-# What k_mpnn<1> executes (node-projection split of the 384-wide first layers)
-MPNN1_EXEC_FLOP_PER_RES = K * 6 * 2 * H * H + 4 * 2 * H * H + 2 * (H * 4 * H + 4 * H * H)
+# What k_mpnn<1> executes: node-projection split of the 384-wide first layers
+# (edge MLP 3 GEMMs of 128x128 per edge, message MLP 2 per edge), the message MLP's last layer
+# once per receiver after the segment sum, the 4 node projections and the node FFN
+MPNN1_EXEC_FLOP_PER_RES = K * 5 * 2 * H * H + 2 * H * H + 4 * 2 * H * H + 2 * (H * 4 * H + 4 * H * H)
 
 
 def parse():
@@ -177,7 +179,7 @@ def main():
         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
         "note": "achieved/frac count SURVEY 8d algorithmic FLOPs; the kernel executes "
                 f"{MPNN1_EXEC_FLOP_PER_RES / MPNN1_ALG_FLOP_PER_RES:.3f}x of them (node-projection split, "
-                "DESIGN.md 5): executed_tflops/peak = frac_executed",
+                "message last layer after the segment sum; DESIGN.md 5): executed_tflops/peak = frac_executed",
         "launch_ms": round(dom_ms, 3),
         "executed_tflops": round(executed, 2),
         "frac_executed": round(executed / PEAK_FP32_TFLOPS, 4),

@@ -420,6 +420,21 @@ typedef struct {
 
 /* Every Linear's fma chain starts from its bias ("bias-first"); the first layer of an edge
  * MLP starts from Ps[s] + Pr[r], where Pr's own chain started from that layer's bias. */
+/* The message MLP up to its last (linear) layer: g = GELU(b1 + GELU(t1)·W1); the last layer
+ * runs once per receiver on the ordered sum of the g rows (msg_agg), since
+ * sum_j (g_j·W2 + b2) = (sum_j g_j)·W2 + deg·b2. */
+static void msg_hidden(float* t1, const lin_t* L, float* g) {
+  for (int c = 0; c < H; ++c) t1[c] = c_gelu(t1[c]);
+  gemv(t1, H, L[1].w, H, H, L[1].b, NULL, g);
+  for (int c = 0; c < H; ++c) g[c] = c_gelu(g[c]);
+}
+
+static void msg_agg(const float* G, int deg, const lin_t* L, float* agg) {
+  float init[H];
+  for (int c = 0; c < H; ++c) init[c] = (float)deg * L[2].b[c];
+  gemv(G, H, L[2].w, H, H, init, NULL, agg);
+}
+
 static void mlp3_tail(float* t1, const lin_t* L, float* y) {
   float t2[H];
   for (int c = 0; c < H; ++c) t1[c] = c_gelu(t1[c]);
@@ -439,12 +454,19 @@ static void mlp3(const float* Ps, const float* Pr, const float* e, const lin_t* 
  * e0 = T[s-r] + f·Wf, the first layer's e-part is U[s-r] + f·Wm, U = T·Wc, Wm = Wf·Wc (Wc = the
  * first layer's rows 256..383), each an fmaf chain in the canonical order; the chain starts from
  * (Ps[s] + Pr[r]) + U[s-r] and runs over the 32 (27 + zero pad) features. */
-static void mlp3_l0(const float* Ps, const float* Pr, const float* U, const float* f32, const float* Wm,
-                    const lin_t* L, float* y) {
+static void msg_hidden_l0(const float* Ps, const float* Pr, const float* U, const float* f32, const float* Wm,
+                          const lin_t* L, float* g) {
   float init[H], t1[H];
   for (int c = 0; c < H; ++c) init[c] = (Ps[c] + Pr[c]) + U[c];
   gemv(f32, 32, Wm, H, H, init, NULL, t1);
-  mlp3_tail(t1, L, y);
+  msg_hidden(t1, L, g);
+}
+
+static void msg_hidden_e(const float* Ps, const float* Pr, const float* e, const lin_t* L, float* g) {
+  float init[H], t1[H];
+  for (int c = 0; c < H; ++c) init[c] = Ps[c] + Pr[c];
+  gemv(e, H, L[0].w + 2 * H * H, H, H, init, NULL, t1);
+  msg_hidden(t1, L, g);
 }
 
 /* node projections of an MLP's first layer: Ps = h W[0:128] (from 0), Pr = b + h W[128:256] */
@@ -520,8 +542,8 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
     }
     for (int i = 0; i < n; ++i) proj2(h + (size_t)i * H, &M->msg[0], Ps + (size_t)i * H, Pr + (size_t)i * H);
     for (int r = 0; r < n; ++r) {
-      float agg[H], m[H], x[H], h1[H], f1[4 * H], f2[H];
-      for (int c = 0; c < H; ++c) agg[c] = 0.0f;
+      float gsum[H], agg[H], m[H], x[H], h1[H], f1[4 * H], f2[H];
+      for (int c = 0; c < H; ++c) gsum[c] = 0.0f;
       for (int j = 0; j < deg[r]; ++j) {
         size_t slot = (size_t)r * k + j;
         int s = senders[slot];
@@ -529,12 +551,13 @@ int pst_oracle_encode(const float* blob, int D, const int32_t* levels, int df, i
           float f32[32];
           memcpy(f32, feat + slot * 32, sizeof(f32));
           for (int c = 27; c < 32; ++c) f32[c] = 0.0f;
-          mlp3_l0(Ps + (size_t)s * H, Pr + (size_t)r * H, Utab + (size_t)(s - r + 511) * H, f32, Wm, M->msg, m);
+          msg_hidden_l0(Ps + (size_t)s * H, Pr + (size_t)r * H, Utab + (size_t)(s - r + 511) * H, f32, Wm, M->msg, m);
         } else {
-          mlp3(Ps + (size_t)s * H, Pr + (size_t)r * H, e + slot * H, M->msg, m);
+          msg_hidden_e(Ps + (size_t)s * H, Pr + (size_t)r * H, e + slot * H, M->msg, m);
         }
-        for (int c = 0; c < H; ++c) agg[c] = agg[c] + m[c];
+        for (int c = 0; c < H; ++c) gsum[c] = gsum[c] + m[c];
       }
+      msg_agg(gsum, deg[r], M->msg, agg);
       for (int c = 0; c < H; ++c) x[c] = h[(size_t)r * H + c] + agg[c] / 50.0f;
       layer_norm(x, M->ln_s[0], M->ln_o[0], h1);
       gemv(h1, H, M->ff[0].w, 4 * H, 4 * H, M->ff[0].b, NULL, f1);

@@ -464,6 +464,40 @@ __device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
   mlp3_tail(acc, W);
 }
 
+// The message MLP up to its last (linear) layer: acc <- GELU(b1 + GELU(acc)·W1). The last layer
+// commutes with the segment sum, sum_j (g_j·W2 + b2) = (sum_j g_j)·W2 + deg·b2, so it runs once
+// per receiver (agg_from_gsum) instead of once per edge.
+__device__ __forceinline__ void msg_hidden(Tile& acc, const MlpW& W) {
+  Tile a2;
+  tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu{});
+  __builtin_amdgcn_sched_barrier(0);
+  // 20 wait states: the packed GELU's asm reads the accumulators the last MFMAs just wrote,
+  // and only the compiler's hazard recognizer would otherwise space them
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3");
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const f32x2 v = c_gelu2_asm<false>((f32x2){a2.m[M][r], a2.m[M][r + 1]});
+      acc.m[M][r] = v.x;
+      acc.m[M][r + 1] = v.y;
+    }
+}
+
+// agg = deg·b2 + G·W2 for the 32 receivers of the tile (G = ordered sums of the hidden rows,
+// perm rows at gsum; lane&31 = receiver with `deg` messages)
+__device__ __forceinline__ void agg_from_gsum(Tile& ag, const float* __restrict__ gsum, int deg, const MlpW& W) {
+  Tile G;
+  tile_load_perm(G, gsum);
+  const float* b2 = W.b2 + (lane_id() >> 5) * 64;
+  const float fd = (float)deg;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ag.m[M][r] = fd * b2[M * 16 + r];
+  tile_gemm(ag, G, W.w2);
+}
+
 // acc += x[features] · Wf over the 32 (27 + zero pad) edge features, 16 MFMA k-steps;
 // x[r] holds features (r&3) + 8(r>>2) + 4·half (the k order of the fragments)
 __device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const float4* __restrict__ Wf) {
@@ -549,10 +583,11 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
     tile_add_rows(m, a.PM0 + (int64_t)ls0 * 256 + 0, a.PM0 + (int64_t)lr0 * 256 + 128);
     tile_add_row(m, a.Utab + (int64_t)(ls0 - lr0 + 511) * 128);
     feat_gemm(m, x, a.W_msg0f);
-    mlp3_tail(m, a.msg);
+    msg_hidden(m, a.msg);
   } else {
     tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
-    mlp3(m, e, a.msg);
+    tile_gemm(m, e, a.msg.w0);
+    msg_hidden(m, a.msg);
   }
 }
 
@@ -565,7 +600,7 @@ __device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t
   Tile x;
   {
     Tile ag;
-    tile_load_perm(ag, aggl + (lane & 31) * 128);
+    agg_from_gsum(ag, aggl + (lane & 31) * 128, a.deg[gl], a.msg);
     if (LAYER == 0) {
       int lr = a.node_local[gl];
       tile_load_perm(x, a.h0tab + (int64_t)(lr < 0 ? 0 : lr) * 128);
@@ -688,7 +723,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   Tile x;
   {
     Tile ag;
-    tile_load_perm(ag, aggl + (lane & 31) * 128);
+    agg_from_gsum(ag, aggl + (lane & 31) * 128, a.deg[gl], a.msg);
     if (LAYER == 0) {
       int lr = a.node_local[gl];
       tile_load_perm(x, a.h0tab + (int64_t)(lr < 0 ? 0 : lr) * 128);
