@@ -34,6 +34,13 @@ bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
   return SPLIT_COST_PER_TASK * (double)n_tasks < fused;
 }
 
+// Downsampler (df 1): a batch of at most this many tiles per SIMD runs k_down_coop (four waves
+// per 32-token tile) instead of k_down (one wave per tile): below that the one-wave kernel
+// leaves most SIMDs idle and its latency is the 20 sequential GEMMs of one wave. Measured
+// (tools/down_coop_ab.sh): 64 tiles 0.34 -> 0.21 ms, 256 tiles 0.41 -> 0.27 ms, 512 tiles equal,
+// 1024 tiles 0.44 -> 0.73 ms.
+constexpr double DOWN_COOP_SIMD_FRACTION = 0.375;
+
 thread_local std::string g_create_error;
 
 
@@ -183,6 +190,7 @@ struct pst_ctx {
   size_t msg_bytes = 0;
   int64_t split_tasks = -2;  // PST_SPLIT_TASKS: split iff n_tasks <= this; -1 = cost model; -2 = not read yet
   int64_t n_simds = 1024;    // 4 x compute units of the device
+  int64_t down_coop = -2;    // PST_DOWN_COOP: k_down_coop iff n_tiles <= this; -1 = default; -2 = not read yet
   std::vector<int64_t> h_offsets;
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
@@ -595,7 +603,12 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   d.bounded_out = w.bounded;
   d.quant_out = w.quant;
   d.pre_proj_out = w.pre_proj;
-  if (d.n_tiles > 0) pst::launch_down(ctx->df, d, st);
+  if (ctx->down_coop == -2) {
+    const char* e = getenv("PST_DOWN_COOP");
+    ctx->down_coop = e ? std::max<int64_t>(0, atoll(e)) : -1;
+  }
+  const int64_t coop_max = ctx->down_coop >= 0 ? ctx->down_coop : (int64_t)(DOWN_COOP_SIMD_FRACTION * ctx->n_simds);
+  if (d.n_tiles > 0) pst::launch_down(ctx->df, d, d.n_tiles <= coop_max, st);
   mark(ctx, 6);
   HIPCHK(hipGetLastError());
   ctx->last_R = R;

@@ -149,7 +149,8 @@ struct FsqAuxArgs {
 void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st);
 void launch_knn(const KnnArgs& a, hipStream_t st);
 void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st);
-void launch_down(int df, const DownArgs& a, hipStream_t st);
+// coop (df 1 only): one workgroup per tile, the GEMMs split over its four waves (small batches)
+void launch_down(int df, const DownArgs& a, bool coop, hipStream_t st);
 void launch_fsq_aux(const FsqAuxArgs& a, int n_prot, hipStream_t st);
 // Y = (init or 0) + X·W (+ b): init / b perm-ordered 128-vectors (either may be null)
 void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, const float* init, float* Y,

@@ -1025,6 +1025,200 @@ __global__ __launch_bounds__(256, DF == 1 ? 2 : 1) void k_down(DownArgs a) {
   }
 }
 
+// ------------------------------------------------------------------- k_down_coop
+// Small-batch form of k_down<1>: one workgroup per 32-token tile, wave w computes output
+// block w (channels 32w … 32w+31) of every GEMM, so a tile's 20 sequential 128x128 GEMMs take
+// a quarter of the MFMA chain latency. Each output channel's fmaf chain is the same one the
+// one-wave kernel runs (same k order, same activation on the B operand), so the bits are equal;
+// full tiles (LayerNorm inputs, next-GEMM operands) are assembled through LDS, double buffered
+// so each exchange costs one barrier. The tracks stay in registers (r_buf / o_buf unused).
+
+// acc (block w) += f(X) · W over K = 128; W fragments as in tile_gemm_f, component w, streamed
+// 16 k-steps ahead (64 ahead measured the same)
+#ifndef PST_COOP_DEPTH
+#define PST_COOP_DEPTH 16
+#endif
+template <typename F>
+__device__ __forceinline__ void blk_gemm_f(f32x16& acc, const Tile& X, const float4* __restrict__ Wf, int w, F&& f) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
+  const int vo = lane_id() * 16 + 4 * w;
+  constexpr int D = PST_COOP_DEPTH;
+  float ring[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) ring[i] = buf_load1(rs, vo, i * 1024);
+#pragma unroll
+  for (int t = 0; t < 64; t += 2) {
+    const f32x2 b = f(t, (f32x2){X.m[t / 16][t % 16], X.m[t / 16][t % 16 + 1]});
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float a = ring[(t + j) % D];
+      if (t + j + D < 64) ring[(t + j) % D] = buf_load1(rs, vo, (t + j + D) * 1024);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, j ? b.y : b.x, acc, 0, 0, 0);
+    }
+  }
+}
+__device__ __forceinline__ void blk_gemm(f32x16& acc, const Tile& X, const float4* __restrict__ Wf, int w) {
+  blk_gemm_f(acc, X, Wf, w, ActId{});
+}
+__device__ __forceinline__ f32x16 blk_pick(const Tile& t, int w) {
+  return w == 0 ? t.m[0] : w == 1 ? t.m[1] : w == 2 ? t.m[2] : t.m[3];
+}
+// v (block w) += vperm (block w)
+__device__ __forceinline__ void blk_add_vec(f32x16& v, const float* __restrict__ vperm, int w) {
+  const float4* p = reinterpret_cast<const float4*>(vperm + (lane_id() >> 5) * 64 + w * 16);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 x = p[q];
+    v[4 * q] = v[4 * q] + x.x;
+    v[4 * q + 1] = v[4 * q + 1] + x.y;
+    v[4 * q + 2] = v[4 * q + 2] + x.z;
+    v[4 * q + 3] = v[4 * q + 3] + x.w;
+  }
+}
+// every wave contributes its block; all waves get the full tile
+__device__ __forceinline__ void blk_exchange(Tile& t, const f32x16& part, float* xs, int& xb, int w) {
+  float* buf = xs + xb * (4 * 16 * 64);
+  xb ^= 1;
+  const int lane = lane_id();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) buf[(w * 16 + r) * 64 + lane] = part[r];
+  __syncthreads();
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t.m[M][r] = buf[(M * 16 + r) * 64 + lane];
+}
+
+__global__ __launch_bounds__(256, 1) void k_down_coop(DownArgs a) {
+  __shared__ float xs[2 * 4 * 16 * 64];
+  int xb = 0;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tile_id = blockIdx.x;
+  if (tile_id >= a.n_tiles) return;  // whole workgroup
+  const int b = a.tile_prot[tile_id];
+  const int t0 = a.tile_t0[tile_id];
+  const int64_t base = a.offsets[b];
+  const int T = a.n_nodes[b];
+  const int t = t0 + (lane & 31);
+  const bool valid = t < T;
+  const int tc = valid ? t : (T > 0 ? T - 1 : 0);
+  Tile r, o;
+  tile_load_perm(r, a.RPE + (int64_t)tc * 128);
+  tile_load_perm(o, a.o_buf + (base + tc) * 128);
+  for (int blk = 0; blk < 3; ++blk) {
+    const DownBlockW& W = a.blk[blk];
+    f32x16 wa = {};
+    {
+      Tile x = o;
+      tile_layer_norm(x, W.dn_s, W.dn_o);
+      blk_gemm(wa, x, W.wv, w);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) wa[i] = wa[i] + 0.0f;  // fmaf(1, v, 0)
+    }
+    {
+      Tile q = r;
+      tile_layer_norm(q, W.qn_s, W.qn_o);
+      f32x16 gt = {};
+      blk_gemm(gt, q, W.wg, w);
+      blk_add_vec(gt, W.gb, w);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) wa[i] = wa[i] * c_sigmoid(gt[i]);
+    }
+    {
+      Tile waf;
+      blk_exchange(waf, wa, xs, xb, w);
+      f32x16 oo = {};
+      blk_gemm(oo, waf, W.wo, w);
+      blk_add_vec(oo, W.ob, w);
+      f32x16 rp = blk_pick(r, w);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) rp[i] = rp[i] + oo[i];
+      blk_exchange(r, rp, xs, xb, w);
+    }
+    {  // resampled transition
+      Tile x = r;
+      tile_layer_norm(x, W.rt_ln_s, W.rt_ln_o);
+      f32x16 acc = {};
+      for (int ck = 0; ck < 2; ++ck) {
+        f32x16 h1 = {};
+        blk_gemm(h1, x, W.rt_w1 + ck * 64 * 64, w);
+        Tile hid;
+        blk_exchange(hid, h1, xs, xb, w);
+        blk_gemm_f(acc, hid, W.rt_w2 + ck * 64 * 64, w, ActBiasRelu{W.rt_b1 + ck * 128});
+      }
+      blk_add_vec(acc, W.rt_b2, w);
+      f32x16 rp = blk_pick(r, w);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) rp[i] = rp[i] + acc[i];
+      blk_exchange(r, rp, xs, xb, w);
+    }
+    if (blk < 2) {  // original transition
+      Tile x = o;
+      tile_layer_norm(x, W.ot_ln_s, W.ot_ln_o);
+      f32x16 acc = {};
+      for (int ck = 0; ck < 2; ++ck) {
+        f32x16 h1 = {};
+        blk_gemm(h1, x, W.ot_w1 + ck * 64 * 64, w);
+        blk_add_vec(h1, W.ot_b1 + ck * 128, w);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) h1[i] = h1[i] > 0.0f ? h1[i] : 0.0f;
+        Tile hid;
+        blk_exchange(hid, h1, xs, xb, w);
+        blk_gemm(acc, hid, W.ot_w2 + ck * 64 * 64, w);
+      }
+      blk_add_vec(acc, W.ot_b2, w);
+      f32x16 op = blk_pick(o, w);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) op[i] = op[i] + acc[i];
+      blk_exchange(o, op, xs, xb, w);
+    }
+  }
+  // spherical norm (every wave, full tile, canonical order)
+  float s = 0.0f;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s = s + r.m[M][q] * r.m[M][q];
+  const float nrm = sqrtf(s + __shfl_xor(s, 32, 64)) + 1e-6f;
+  const int h = lane >> 5;
+  const int64_t orow_i = base + t;
+  if (valid) {  // continuous_embedding_pre_proj, block w, natural channel order
+    f32x16 rn = blk_pick(r, w);
+    float4* pp = reinterpret_cast<float4*>(a.pre_proj_out + orow_i * 128);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      pp[(32 * w + 8 * q + 4 * h) / 4] =
+          make_float4(rn[4 * q] / nrm, rn[4 * q + 1] / nrm, rn[4 * q + 2] / nrm, rn[4 * q + 3] / nrm);
+  }
+  if (w != 0) return;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) r.m[M][q] = r.m[M][q] / nrm;
+  f32x16 z;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) z[q] = 0.0f;
+  tile_gemm_narrow(z, r, a.down_w);
+  uint32_t part_idx = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int d = q + 4 * h;
+    if (d < a.D) {
+      float zz = z[q] + a.down_b[d];
+      float bnd = c_tanh(zz + a.fsq_shift[d]) * a.fsq_half[d] - a.fsq_off[d];
+      float qv = rintf(bnd);
+      part_idx += (uint32_t)((int)qv + a.fsq_L[d] / 2) * (uint32_t)a.fsq_basis[d];
+      if (valid) {
+        a.bounded_out[orow_i * 8 + d] = bnd;
+        a.quant_out[orow_i * 8 + d] = qv;
+      }
+    }
+  }
+  uint32_t idx = part_idx + (uint32_t)__shfl_xor((int)part_idx, 32, 64);
+  if (valid && h == 0) a.tokens_out[orow_i] = idx;
+}
+
 // ---------------------------------------------------------------------------- tables
 // Y[row] = X[row] · W (+ b); rows of X and Y in perm order, 32 rows per wave.
 __global__ __launch_bounds__(256) void k_table_gemm(const float* __restrict__ X, int n_rows,
@@ -1072,9 +1266,10 @@ void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st) {
   else if (layer == 1) hipLaunchKernelGGL(k_mpnn<1>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(k_mpnn<2>, grid, dim3(256), 0, st, a);
 }
-void launch_down(int df, const DownArgs& a, hipStream_t st) {
+void launch_down(int df, const DownArgs& a, bool coop, hipStream_t st) {
   dim3 grid((unsigned)((a.n_tiles + 3) / 4));
-  if (df == 1) hipLaunchKernelGGL(k_down<1>, grid, dim3(256), 0, st, a);
+  if (df == 1 && coop) hipLaunchKernelGGL(k_down_coop, dim3((unsigned)a.n_tiles), dim3(256), 0, st, a);
+  else if (df == 1) hipLaunchKernelGGL(k_down<1>, grid, dim3(256), 0, st, a);
   else if (df == 2) hipLaunchKernelGGL(k_down<2>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(k_down<4>, grid, dim3(256), 0, st, a);
 }

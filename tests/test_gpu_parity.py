@@ -252,6 +252,30 @@ def test_fused_and_split_layers_identical(split, monkeypatch):
     assert np.array_equal(tok[off[2]: off[2] + nt[2]], o["tokens"])
 
 
+@pytest.mark.parametrize("cb", [4096, 64000])
+def test_down_coop_and_one_wave_identical(cb, monkeypatch):
+    """k_down_coop (four waves per 32-token tile, small batches) and k_down<1> (one wave per
+    tile) give the same bits: tokens, bounded/quantized codes and pre-projection embeddings."""
+    from pst_amd._native import Tokenizer, pack_samples
+    samples = [synthetic.synthetic_protein(n, 700 + n) for n in (51, 64, 200, 512, 97)]
+    pos, flags, off = pack_samples(samples)
+    R = int(off[-1])
+    blob = P.random_blob(len(LEVELS[cb]), 77)
+    outs = []
+    for coop in ("0", "1000000"):
+        monkeypatch.setenv("PST_DOWN_COOP", coop)
+        tk = Tokenizer(0, cb, 1, blob)
+        tok, nt, _ = tk.tokenize_packed(pos, flags, off)
+        outs.append((tok[:R].copy(), tk.aux(R)))
+    (t0, a0), (t1, a1) = outs
+    assert np.array_equal(t0, t1)
+    for k in ("bounded", "quantize", "pre_proj"):
+        assert np.array_equal(a0[k].view(np.uint32), a1[k].view(np.uint32)), k
+    s = samples[3]
+    o = O.tokenize(blob, LEVELS[cb], 1, s.atom37_positions, s.atom_flags())
+    assert np.array_equal(t1[off[3]: off[3] + nt[3]], o["tokens"])
+
+
 def test_build_graph_matches_reference_padded_graphs():
     """pst_build_graph + the host padding == the reference's preprocess_sample(...).graph for
     every graph_golden case, in one ragged batch (edge features bitwise as float32)."""
