@@ -40,6 +40,9 @@ bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
 // (tools/down_coop_ab.sh): 64 tiles 0.34 -> 0.21 ms, 256 tiles 0.41 -> 0.27 ms, 512 tiles equal,
 // 1024 tiles 0.44 -> 0.73 ms.
 constexpr double DOWN_COOP_SIMD_FRACTION = 0.375;
+// Split-schedule node update: k_mpnn_node_coop (four waves per 32 receivers) up to this many
+// tasks per SIMD, k_mpnn_node (one wave) above.
+constexpr double NODE_COOP_SIMD_FRACTION = 0.375;
 
 thread_local std::string g_create_error;
 
@@ -190,6 +193,7 @@ struct pst_ctx {
   size_t msg_bytes = 0;
   int64_t split_tasks = -2;  // PST_SPLIT_TASKS: split iff n_tasks <= this; -1 = cost model; -2 = not read yet
   int64_t n_simds = 1024;    // 4 x compute units of the device
+  int64_t node_coop = -2;    // PST_NODE_COOP: k_mpnn_node_coop iff split and n_tasks <= this; -1 = default
   int64_t down_coop = -2;    // PST_DOWN_COOP: k_down_coop iff n_tiles <= this; -1 = default; -2 = not read yet
   std::vector<int64_t> h_offsets;
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
@@ -496,6 +500,12 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     ctx->split_tasks = e ? std::max<int64_t>(0, atoll(e)) : -1;
   }
   const bool split = ctx->split_tasks >= 0 ? n_tasks <= ctx->split_tasks : use_split_schedule(n_tasks, ctx->n_simds);
+  if (ctx->node_coop == -2) {
+    const char* e = getenv("PST_NODE_COOP");
+    ctx->node_coop = e ? std::max<int64_t>(0, atoll(e)) : -1;
+  }
+  const bool node_coop =
+      split && n_tasks <= (ctx->node_coop >= 0 ? ctx->node_coop : (int64_t)(NODE_COOP_SIMD_FRACTION * ctx->n_simds));
   float* msg_rows = nullptr;
   int32_t bpw = 1;
   if (split) {
@@ -562,7 +572,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.e_out = ebuf[l];
     m.h_out = hbuf[l + 1];
     m.P_out = pbuf[l];
-    pst::launch_mpnn(l, m, st);
+    pst::launch_mpnn(l, m, node_coop, st);
     mark(ctx, 3 + l);
     if (ctx->dbg[l]) HIPCHK(hipMemcpyAsync(ctx->dbg[l], m.h_out, sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
   }

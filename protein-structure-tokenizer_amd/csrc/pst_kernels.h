@@ -148,7 +148,8 @@ struct FsqAuxArgs {
 
 void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st);
 void launch_knn(const KnnArgs& a, hipStream_t st);
-void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st);
+// node_coop (split schedule only): node update as k_mpnn_node_coop, four waves per 32 receivers
+void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st);
 // coop (df 1 only): one workgroup per tile, the GEMMs split over its four waves (small batches)
 void launch_down(int df, const DownArgs& a, bool coop, hipStream_t st);
 void launch_fsq_aux(const FsqAuxArgs& a, int n_prot, hipStream_t st);

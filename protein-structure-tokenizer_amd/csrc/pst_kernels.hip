@@ -1219,6 +1219,117 @@ __global__ __launch_bounds__(256, 1) void k_down_coop(DownArgs a) {
   if (valid && h == 0) a.tokens_out[orow_i] = idx;
 }
 
+// ------------------------------------------------------------- k_mpnn_node_coop
+// Small-batch node update (split schedule): one workgroup per 32 receivers, wave w owns output
+// channels 32w … 32w+31 of each of the 13 GEMMs (node_update's chains, same order), full tiles
+// assembled through LDS as in k_down_coop. The FFN's GELU is applied to a wave's own block
+// before the exchange (elementwise, same function), so it is not evaluated four times.
+
+// acc (block w) = bias + f(X)·W (tile_gemm_bf for one output block)
+template <typename F>
+__device__ __forceinline__ void blk_gemm_bf(f32x16& acc, const Tile& X, const float4* __restrict__ Wf,
+                                            const float4* __restrict__ Bf, int w, F&& f) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Bf);
+  const float bb = buf_load1(rs, lane_id() * 16 + 4 * w, 0);
+  const float one = lane_id() < 32 ? 1.0f : 0.0f;
+  const f32x16 z = {};
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bb, one, z, 0, 0, 0);
+  blk_gemm_f(acc, X, Wf, w, f);
+}
+// this lane's block-w values of a perm row
+__device__ __forceinline__ f32x16 blk_load_row(const float* __restrict__ row, int w) {
+  const float4* p = reinterpret_cast<const float4*>(row + (lane_id() >> 5) * 64 + w * 16);
+  f32x16 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 x = p[q];
+    v[4 * q] = x.x;
+    v[4 * q + 1] = x.y;
+    v[4 * q + 2] = x.z;
+    v[4 * q + 3] = x.w;
+  }
+  return v;
+}
+__device__ __forceinline__ void blk_store_row(const f32x16& v, float* __restrict__ row, int w) {
+  float4* p = reinterpret_cast<float4*>(row + (lane_id() >> 5) * 64 + w * 16);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+template <int LAYER>
+__global__ __launch_bounds__(256, 1) void k_mpnn_node_coop(MpnnArgs a) {
+  __shared__ float xs[2 * 4 * 16 * 64];
+  int xb = 0;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t task = blockIdx.x;
+  if (task >= a.n_tasks) return;  // whole workgroup
+  const int64_t gl = task * 32 + (lane & 31);
+  Tile x;
+  {
+    // agg = deg·b2 + G·W2 (agg_from_gsum), block w
+    f32x16 ag;
+    const float* b2 = a.msg.b2 + (lane >> 5) * 64 + w * 16;
+    const float fd = (float)a.deg[gl];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ag[r] = fd * b2[r];
+    Tile G;
+    tile_load_perm(G, a.agg + gl * 128);
+    blk_gemm(ag, G, a.msg.w2, w);
+    const float* hrow;
+    if (LAYER == 0) {
+      const int lr = a.node_local[gl];
+      hrow = a.h0tab + (int64_t)(lr < 0 ? 0 : lr) * 128;
+    } else {
+      hrow = a.h_in + gl * 128;
+    }
+    f32x16 xp = blk_load_row(hrow, w);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xp[r] = xp[r] + ag[r] / 50.0f;
+    blk_exchange(x, xp, xs, xb, w);
+  }
+  tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0
+  f32x16 out;
+  for (int ck = 0; ck < 4; ++ck) {
+    f32x16 h1;
+    blk_gemm_bf(h1, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, w, ActId{});
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const f32x2 v = c_gelu2((f32x2){h1[r], h1[r + 1]});
+      h1[r] = v.x;
+      h1[r + 1] = v.y;
+    }
+    Tile hid;
+    blk_exchange(hid, h1, xs, xb, w);
+    if (ck == 0)
+      blk_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, w, ActId{});
+    else
+      blk_gemm(out, hid, a.ff_w2 + ck * 64 * 64, w);
+  }
+  {
+    f32x16 xp = blk_pick(x, w);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xp[r] = xp[r] + out[r];
+    blk_exchange(x, xp, xs, xb, w);
+  }
+  tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
+  blk_store_row(blk_pick(x, w), a.h_out + gl * 128, w);
+  if (a.P_out) {
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+      f32x16 pr;
+      if (p & 1) {
+        blk_gemm_bf(pr, x, a.proj_w + p * 64 * 64, a.proj_bf[p >> 1], w, ActId{});
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pr[r] = 0.0f;
+        blk_gemm(pr, x, a.proj_w + p * 64 * 64, w);
+      }
+      blk_store_row(pr, a.P_out + gl * 512 + p * 128, w);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- tables
 // Y[row] = X[row] · W (+ b); rows of X and Y in perm order, 32 rows per wave.
 __global__ __launch_bounds__(256) void k_table_gemm(const float* __restrict__ X, int n_rows,
@@ -1247,7 +1358,7 @@ void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st) {
 void launch_knn(const KnnArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_knn, dim3((unsigned)((a.n_slots + 3) / 4)), dim3(256), 0, st, a);
 }
-void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st) {
+void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st) {
   dim3 grid((unsigned)((a.n_tasks + 3) / 4));
   if (a.msg_rows) {  // split mode
     const int64_t waves = (a.n_tasks * 50 + a.blocks_per_wave - 1) / a.blocks_per_wave;
@@ -1257,7 +1368,11 @@ void launch_mpnn(int layer, const MpnnArgs& a, hipStream_t st) {
     else hipLaunchKernelGGL(k_mpnn_edge<2>, egrid, dim3(256), 0, st, a);
     const int64_t rows = a.n_tasks * 32;
     hipLaunchKernelGGL(k_seg_sum, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a.msg_rows, a.deg, a.agg, rows);
-    if (layer == 0) hipLaunchKernelGGL(k_mpnn_node<0>, grid, dim3(256), 0, st, a);
+    const dim3 cgrid((unsigned)a.n_tasks);
+    if (node_coop && layer == 0) hipLaunchKernelGGL(k_mpnn_node_coop<0>, cgrid, dim3(256), 0, st, a);
+    else if (node_coop && layer == 1) hipLaunchKernelGGL(k_mpnn_node_coop<1>, cgrid, dim3(256), 0, st, a);
+    else if (node_coop) hipLaunchKernelGGL(k_mpnn_node_coop<2>, cgrid, dim3(256), 0, st, a);
+    else if (layer == 0) hipLaunchKernelGGL(k_mpnn_node<0>, grid, dim3(256), 0, st, a);
     else if (layer == 1) hipLaunchKernelGGL(k_mpnn_node<1>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_mpnn_node<2>, grid, dim3(256), 0, st, a);
     return;

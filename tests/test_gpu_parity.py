@@ -276,6 +276,31 @@ def test_down_coop_and_one_wave_identical(cb, monkeypatch):
     assert np.array_equal(t1[off[3]: off[3] + nt[3]], o["tokens"])
 
 
+def test_node_coop_and_one_wave_identical(monkeypatch):
+    """Split schedule: k_mpnn_node_coop (four waves per 32 receivers) and k_mpnn_node (one wave)
+    give the same node features after every layer and the same tokens."""
+    from pst_amd._native import Tokenizer, pack_samples
+    samples = [synthetic.synthetic_protein(n, 900 + n) for n in (50, 77, 256, 512, 130)]
+    pos, flags, off = pack_samples(samples)
+    R = int(off[-1])
+    blob = P.random_blob(6, 1234)
+    monkeypatch.setenv("PST_SPLIT_TASKS", "1000000")
+    monkeypatch.setenv("PST_DEBUG", "1")
+    outs = []
+    for coop in ("0", "1000000"):
+        monkeypatch.setenv("PST_NODE_COOP", coop)
+        tk = Tokenizer(0, 4096, 1, blob)
+        tok, nt, _ = tk.tokenize_packed(pos, flags, off)
+        outs.append((tok[:R].copy(), [tk.debug_fetch(w, R) for w in (1, 2, 3)]))
+    (t0, h0), (t1, h1) = outs
+    for a, b in zip(h0, h1):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(t0, t1)
+    s = samples[2]
+    o = O.tokenize(blob, LEVELS[4096], 1, s.atom37_positions, s.atom_flags())
+    assert np.array_equal(t1[off[2]: off[2] + nt[2]], o["tokens"])
+
+
 def test_build_graph_matches_reference_padded_graphs():
     """pst_build_graph + the host padding == the reference's preprocess_sample(...).graph for
     every graph_golden case, in one ragged batch (edge features bitwise as float32)."""
