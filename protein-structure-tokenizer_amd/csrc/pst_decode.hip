@@ -577,29 +577,57 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   }
   __syncthreads();
   float* f = feat + ig * 2112;
-  // scalar values (192) and global value points (288)
+  // scalar values (192) and global value points (288); the key loops are unrolled 8-wide with
+  // the 8 loads issued ahead of the (in-order) fmaf chain, so a thread keeps 8 loads in flight
   for (int o = tid; o < 192 + 288; o += 256) {
-    float acc = 0.0f;
+    int h, q = 0;
+    const float* src;
+    int64_t stride;
     if (o < 192) {
-      const int h = o / 16, c = o % 16;
-      for (int j = 0; j < N; ++j) acc = __builtin_fmaf(att[h][j], kvs[(int64_t)j * 384 + h * 32 + 16 + c], acc);
-      f[o] = acc;
+      h = o / 16;
+      src = kvs + h * 32 + 16 + o % 16;
+      stride = 384;
     } else {
-      const int q = o - 192, h = q / 24, p = (q / 3) % 8, xyz = q % 3;
-      for (int j = 0; j < N; ++j)
-        acc = __builtin_fmaf(att[h][j], kvpg[(((int64_t)j * 12 + h) * 12 + 4 + p) * 3 + xyz], acc);
-      res_pt[q] = acc;
+      q = o - 192;
+      h = q / 24;
+      src = kvpg + (h * 12 + 4 + (q / 3) % 8) * 3 + q % 3;
+      stride = 432;
     }
+    const float* arow = att[h];
+    float acc = 0.0f;
+    int j = 0;
+    for (; j + 8 <= N; j += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(j + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = __builtin_fmaf(arow[j + u], v[u], acc);
+    }
+    for (; j < N; ++j) acc = __builtin_fmaf(arow[j], src[(int64_t)j * stride], acc);
+    if (o < 192)
+      f[o] = acc;
+    else
+      res_pt[q] = acc;
   }
   // attention over the pair representation: thread → channel c, heads hg, hg+2, ...
   {
     const int c = tid & 127, hg = tid >> 7;
     float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const float* zr = zln + c;
-    for (int j = 0; j < N; ++j) {
+    int j = 0;
+    for (; j + 8 <= N; j += 8) {
+      float zv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) zv[u] = zr[(int64_t)(j + u) * 128];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) acc[k] = __builtin_fmaf(att[hg + 2 * k][j + u], zv[u], acc[k]);
+    }
+    for (; j < N; ++j) {
       const float zv = zr[(int64_t)j * 128];
 #pragma unroll
-      for (int u = 0; u < 6; ++u) acc[u] = __builtin_fmaf(att[hg + 2 * u][j], zv, acc[u]);
+      for (int k = 0; k < 6; ++k) acc[k] = __builtin_fmaf(att[hg + 2 * k][j], zv, acc[k]);
     }
 #pragma unroll
     for (int u = 0; u < 6; ++u) f[576 + (hg + 2 * u) * 128 + c] = acc[u];
