@@ -463,9 +463,31 @@ class DecodeFn:
         self._pool.shutdown(wait=True)
 
 
-def shard_for_rank(items: Sequence[Any], rank: int, world_size: int) -> List[Any]:
-    """Round-robin partition of independent proteins across ranks (one process per GPU, no
-    data-path collective): rank r takes items r, r+W, r+2W, ..."""
+def lpt_partition(weights: Sequence[float], world_size: int) -> List[List[int]]:
+    """Longest-processing-time-first assignment: items by weight, heaviest first
+    (ties by index), each to the currently least-loaded rank (ties to the lowest rank). Returns
+    per-rank index lists in input order. Deterministic, so every rank computes the same split."""
+    if world_size < 1:
+        raise ValueError(f"world size {world_size} < 1")
+    load = [0.0] * world_size
+    parts: List[List[int]] = [[] for _ in range(world_size)]
+    for i in sorted(range(len(weights)), key=lambda k: (-float(weights[k]), k)):
+        r = min(range(world_size), key=lambda q: (load[q], q))
+        parts[r].append(i)
+        load[r] += float(weights[i])
+    return [sorted(p) for p in parts]
+
+
+def shard_for_rank(items: Sequence[Any], rank: int, world_size: int,
+                   weights: Optional[Sequence[float]] = None) -> List[Any]:
+    """Partition of independent proteins across ranks (one process per GPU, no data-path
+    collective). With `weights` (residue counts, or PDB file sizes as their proxy) the split is
+    LPT-greedy on them (`lpt_partition`), balancing residues per GPU; without, round-robin:
+    rank r takes items r, r+W, r+2W, ..."""
     if not 0 <= rank < world_size:
         raise ValueError(f"rank {rank} outside world of {world_size}")
-    return list(items[rank::world_size])
+    if weights is None:
+        return list(items[rank::world_size])
+    if len(weights) != len(items):
+        raise ValueError(f"{len(weights)} weights for {len(items)} items")
+    return [items[i] for i in lpt_partition(weights, world_size)[rank]]

@@ -42,7 +42,9 @@ def main(pdbs: List[str], token_save_path: str, backend: str, batch_size_per_dev
     if world > 1:
         rank = int(os.environ.get("RANK", "0"))
         local_devices = [int(os.environ.get("LOCAL_RANK", "0"))]
-        pdbs = shard_for_rank(sorted(pdbs), rank, world)
+        # LPT on PDB text size (∝ atoms ∝ residues) balances residues per GPU
+        pdbs = sorted(pdbs)
+        pdbs = shard_for_rank(pdbs, rank, world, weights=[os.path.getsize(p) for p in pdbs])
         if not pdbs:
             return
     tokenize = runner.prepare_tokenize_fn(cfg=cfg, devices=local_devices)

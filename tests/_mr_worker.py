@@ -24,7 +24,8 @@ def run(rank, world, port, pdb_dir, model_dir, out_dir, result_q):
     runner.InferenceRunner.prepare_tokenize_fn = staticmethod(lambda cfg, devices: OracleTokenizeFn(cfg, devices))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pdbs = [os.path.join(pdb_dir, f) for f in os.listdir(pdb_dir)]
-    mine = runner.shard_for_rank(sorted(pdbs), rank, world)
+    pdbs_sorted = sorted(pdbs)
+    mine = runner.shard_for_rank(pdbs_sorted, rank, world, weights=[os.path.getsize(p) for p in pdbs_sorted])
     cli.main(pdbs=pdbs, token_save_path=out_dir, backend="gpu", batch_size_per_device=2,
              codebook_size=4096, downsampling_ratio=1, weights_dir=model_dir)
     # host-side gather of what each rank handled (test bookkeeping only, not the data path)

@@ -210,6 +210,26 @@ def test_shard_for_rank_partitions():
         runner.shard_for_rank(items, 3, 3)
 
 
+def test_lpt_partition_balances_residues():
+    """LPT: heaviest first onto the least-loaded rank; a disjoint cover, input order
+    kept inside a shard, and the max load within the LPT bound (4/3 - 1/(3W)) of the optimum."""
+    rng = np.random.default_rng(0)
+    w = rng.integers(50, 513, 97).tolist()
+    for W in (1, 2, 3, 8):
+        parts = runner.lpt_partition(w, W)
+        assert sorted(sum(parts, [])) == list(range(len(w)))
+        assert all(p == sorted(p) for p in parts)
+        loads = [sum(w[i] for i in p) for p in parts]
+        lower = max(sum(w) / W, max(w))
+        assert max(loads) <= (4 / 3 - 1 / (3 * W)) * lower + 1e-9
+    # exact small case: 7,6,5,4,3 on 2 ranks -> {7,4,3}=14 / {6,5}=11 greedy
+    assert runner.lpt_partition([7, 6, 5, 4, 3], 2) == [[0, 3, 4], [1, 2]]
+    items = list("abcde")
+    assert runner.shard_for_rank(items, 1, 2, weights=[7, 6, 5, 4, 3]) == ["b", "c"]
+    with pytest.raises(ValueError):
+        runner.shard_for_rank(items, 0, 2, weights=[1, 2])
+
+
 # ------------------------------------------------------------------------------ native parser
 def _both(txt, chain_id=None):
     from pst_amd import _native
