@@ -197,8 +197,8 @@ class TokenizeFn:
                                                                       *res[0][2][key].shape[1:])
             # perplexity: mean of the per-device normalised histograms (jax.lax.pmean,
             # quantize.py:222-224), replicated per device like the reference's output
-            p = np.mean([r[2]["histogram"] / max(r[2]["histogram"].sum(), 1) for r in res], axis=0)
-            ppl = float(np.exp(-np.sum(p * np.log(p + 1e-10))))
+            p = np.mean([_normalised(r[2]["histogram"]) for r in res], axis=0)
+            ppl = _perplexity(p)
             out["perplexity"] = np.full(n_dev, ppl, np.float32)
             out["straight_through_quantized"] = out["quantize"]
         return out
@@ -461,6 +461,33 @@ class DecodeFn:
             d.close()
         self._ctx.clear()
         self._pool.shutdown(wait=True)
+
+
+def _normalised(histogram: np.ndarray) -> np.ndarray:
+    h = np.asarray(histogram, np.float64)
+    return h / max(h.sum(), 1.0)
+
+
+def _perplexity(p: np.ndarray) -> float:
+    """exp(-Σ p log(p + 1e-10)) of the mean normalised code histogram (quantize.py:222-224)."""
+    return float(np.exp(-np.sum(p * np.log(p + 1e-10))))
+
+
+def global_perplexity(histogram: np.ndarray, group=None) -> float:
+    """Codebook perplexity over all ranks of a torchrun job: the reference's pmean of per-device
+    normalised histograms (quantize.py:222-224) as ONE all-reduce of K float64 (RCCL over xGMI
+    with the nccl backend, gloo on CPU). The only collective of the tokenize path, off the
+    token data path. Without an initialised process group it is the local perplexity."""
+    p = _normalised(histogram)
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        import torch
+        t = torch.from_numpy(p)
+        if dist.get_backend(group) == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, group=group)
+        p = t.cpu().numpy() / dist.get_world_size(group)
+    return _perplexity(p)
 
 
 def lpt_partition(weights: Sequence[float], world_size: int) -> List[List[int]]:

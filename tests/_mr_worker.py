@@ -35,3 +35,18 @@ def run(rank, world, port, pdb_dir, model_dir, out_dir, result_q):
     if rank == 0:
         result_q.put(got)
     dist.destroy_process_group()
+
+
+def run_ppl(rank, world, port, hists, result_q):
+    """global_perplexity over `world` gloo ranks, rank r holding hists[r]."""
+    import torch.distributed as dist
+    from pst_amd import runner
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    v = runner.global_perplexity(hists[rank])
+    got = [None] * world
+    dist.all_gather_object(got, v)
+    if rank == 0:
+        result_q.put(got)
+    dist.destroy_process_group()

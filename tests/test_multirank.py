@@ -1,5 +1,6 @@
-"""N>1 path on CPU: two gloo ranks (127.0.0.1), each takes GPU LOCAL_RANK's round-robin shard of
-the PDB list through the CLI; the union of their token files must equal a single-process run."""
+"""N>1 path on CPU: two gloo ranks (127.0.0.1), each takes GPU LOCAL_RANK's LPT shard of the PDB
+list through the CLI; the union of their token files must equal a single-process run. Plus the
+cross-rank codebook perplexity (the one collective: an all-reduce of K float64)."""
 import multiprocessing as mp
 import os
 import socket
@@ -51,3 +52,25 @@ def test_two_rank_cli_sharding(tmp_path):
         t = np.load(out / f"{k}_tokens.npy")
         want = O.tokenize(blob, (4,) * 6, 1, s.atom37_positions, s.atom_flags())["tokens"]
         assert np.array_equal(t[0], want)
+
+
+def test_global_perplexity_two_ranks():
+    """The cross-rank perplexity (one all-reduce) equals the single-process pmean formula."""
+    import _mr_worker
+    from pst_amd import runner
+    rng = np.random.default_rng(5)
+    hists = [rng.integers(0, 9, 4096).astype(np.uint32), rng.integers(0, 3, 4096).astype(np.uint32)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mr_worker.run_ppl, args=(r, 2, port, hists, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = runner._perplexity(np.mean([runner._normalised(h) for h in hists], axis=0))
+    assert got[0] == got[1]
+    assert abs(got[0] - want) <= 1e-9 * want
+    assert runner.global_perplexity(hists[0]) == runner._perplexity(runner._normalised(hists[0]))
