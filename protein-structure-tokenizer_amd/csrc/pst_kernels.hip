@@ -1160,12 +1160,12 @@ __global__ __launch_bounds__(256, 1) void k_down_coop(DownArgs a) {
       for (int ck = 0; ck < 2; ++ck) {
         f32x16 h1 = {};
         blk_gemm(h1, x, W.ot_w1 + ck * 64 * 64, w);
-        blk_add_vec(h1, W.ot_b1 + ck * 128, w);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) h1[i] = h1[i] > 0.0f ? h1[i] : 0.0f;
+        // bias + ReLU on the B operand after the exchange (the same two ops as k_down's add_vec
+        // + relu): applying them to the wave's block before the exchange, or loading biases
+        // ahead of the GEMMs, measured 20-100 % slower
         Tile hid;
         blk_exchange(hid, h1, xs, xb, w);
-        blk_gemm(acc, hid, W.ot_w2 + ck * 64 * 64, w);
+        blk_gemm_f(acc, hid, W.ot_w2 + ck * 64 * 64, w, ActBiasRelu{W.ot_b1 + ck * 128});
       }
       blk_add_vec(acc, W.ot_b2, w);
       f32x16 op = blk_pick(o, w);
