@@ -19,7 +19,11 @@
 #include <string>
 #include <vector>
 
+#include <hipblaslt/hipblaslt.h>
 #include <rocblas/rocblas.h>
+
+#include <array>
+#include <map>
 
 #include "../../include/pst.h"
 #include "pst_backbone_tables.h"
@@ -771,6 +775,18 @@ struct pst_decoder {
   float* d_pe_rel = nullptr;   // PE(d; 512), d = -511..511 [1023][128]
   float* d_pw = nullptr;       // IPA point weights [12]
   rocblas_handle blas = nullptr;  // library GEMMs (per-node rows; pair rows only when unfused)
+  // hipBLASLt GEMMs with the bias / ReLU epilogue fused (see gemm_any); plans cached per shape
+  struct LtPlan {
+    hipblasLtMatmulDesc_t desc = nullptr;
+    hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
+    hipblasLtMatmulAlgo_t algo{};
+    size_t ws = 0;
+    bool ok = false;
+  };
+  hipblasLtHandle_t lt = nullptr;
+  void* lt_ws = nullptr;
+  size_t lt_ws_bytes = 0;
+  std::map<std::array<int64_t, 7>, LtPlan> lt_plans;
   DecWeights W{};
   float* d_pair = nullptr;  // fused pair kernel: fragments, perm vectors, U table (k_pair_fused)
   PairArgs pair{};          // pointers into d_pair (per-call fields filled by decode_group)
@@ -894,6 +910,42 @@ __global__ __launch_bounds__(256) void k_relu_copy(const float* __restrict__ X, 
   }
 }
 
+thread_local pst_decoder* t_lt = nullptr;  // decoder whose hipBLASLt state gemm_any uses
+
+// plan (descriptor, layouts, heuristic algorithm) for D[N×M] = act(Wᵀ·Xᵀ + β·C + b), column-major
+pst_decoder::LtPlan* lt_plan(pst_decoder* d, int M, int N, int K, int ldx, int ldy, hipblasLtEpilogue_t ep,
+                             bool accum) {
+  const std::array<int64_t, 7> key{M, N, K, ldx, ldy, (int64_t)ep, accum ? 1 : 0};
+  auto it = d->lt_plans.find(key);
+  if (it != d->lt_plans.end()) return it->second.ok ? &it->second : nullptr;
+  pst_decoder::LtPlan& p = d->lt_plans[key];
+  if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+  const uint32_t epv = (uint32_t)ep;
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epv, sizeof(epv));
+  if (ep == HIPBLASLT_EPILOGUE_BIAS || ep == HIPBLASLT_EPILOGUE_RELU_BIAS) {
+    const hipDataType bt = HIP_R_32F;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  }
+  if (hipblasLtMatrixLayoutCreate(&p.a, HIP_R_32F, N, K, N) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p.b, HIP_R_32F, K, M, ldx) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p.c, HIP_R_32F, N, M, ldy) != HIPBLAS_STATUS_SUCCESS)
+    return nullptr;
+  hipblasLtMatmulPreference_t pref = nullptr;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+  const uint64_t wsb = d->lt_ws_bytes;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
+  hipblasLtMatmulHeuristicResult_t res[1];
+  int n = 0;
+  const hipblasStatus_t hs =
+      hipblasLtMatmulAlgoGetHeuristic(d->lt, p.desc, p.a, p.b, p.c, p.c, pref, 1, res, &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (hs != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].workspaceSize > d->lt_ws_bytes) return nullptr;
+  p.algo = res[0].algo;
+  p.ws = res[0].workspaceSize;
+  p.ok = true;
+  return &p;
+}
+
 inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, int K, int N, const float* b, float* Y,
                      int ldy, int M, int flags) {
   if (t_blas && (!(flags & F_RELU_IN) || (int64_t)M * K <= 512 * 2112)) {
@@ -903,6 +955,20 @@ inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, i
       ldx = K;
     }
     const float one = 1.0f, beta = (flags & F_ACCUM) ? 1.0f : 0.0f;
+    // hipBLASLt with the bias / ReLU fused into the GEMM epilogue: act(X·W + β·Y + b), the same
+    // expression the rocBLAS + k_bias_act pair below evaluates in two launches
+    if (t_lt && !(flags & F_SIGMOID_OUT)) {
+      const bool relu = flags & F_RELU_OUT;
+      const hipblasLtEpilogue_t ep = b ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS)
+                                       : (relu ? HIPBLASLT_EPILOGUE_RELU : HIPBLASLT_EPILOGUE_DEFAULT);
+      pst_decoder::LtPlan* p = lt_plan(t_lt, M, N, K, ldx, ldy, ep, flags & F_ACCUM);
+      if (p) {
+        if (b) hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &b, sizeof(b));
+        if (hipblasLtMatmul(t_lt->lt, p->desc, &one, Wt, p->a, X, p->b, &beta, Y, p->c, Y, p->c, &p->algo,
+                            t_lt->lt_ws, p->ws, st) == HIPBLAS_STATUS_SUCCESS)
+          return;
+      }
+    }
     rocblas_sgemm(t_blas, rocblas_operation_none, rocblas_operation_none, N, M, K, &one, Wt, N, X, ldx, &beta, Y, ldy);
     if (b || (flags & (F_RELU_OUT | F_SIGMOID_OUT))) {
       hipLaunchKernelGGL(k_bias_act, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, Y, ldy, b, (int64_t)M, N,
@@ -1000,6 +1066,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   hipStream_t st = dec->stream;
   const int64_t T = G.T, N = G.N, NP = G.NP;
   t_blas = getenv("PST_DECODE_NO_BLAS") ? nullptr : dec->blas;
+  t_lt = (t_blas && dec->lt && !getenv("PST_DECODE_NO_LT")) ? dec : nullptr;
   t_relu_buf = S.relu_buf;
   DCHK(hipMemcpyAsync(S.tokens, G.tokens.data(), sizeof(uint32_t) * T, hipMemcpyHostToDevice, st));
   DCHK(hipMemcpyAsync(S.tok_off, G.tok_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
@@ -1257,6 +1324,14 @@ int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* 
   if (rocblas_create_handle(&dec->blas) != rocblas_status_success ||
       rocblas_set_stream(dec->blas, dec->stream) != rocblas_status_success)
     return bad("rocblas handle creation failed");
+  // hipBLASLt is optional: without it (or a plan for a shape) the rocBLAS path runs
+  dec->lt_ws_bytes = (size_t)32 << 20;
+  if (hipblasLtCreate(&dec->lt) != HIPBLAS_STATUS_SUCCESS || hipMalloc(&dec->lt_ws, dec->lt_ws_bytes) != hipSuccess) {
+    if (dec->lt) (void)hipblasLtDestroy(dec->lt);
+    dec->lt = nullptr;
+    dec->lt_ws = nullptr;
+    dec->lt_ws_bytes = 0;
+  }
   if (hipMalloc(&dec->d_blob, n_params * sizeof(float)) != hipSuccess ||
       hipMemcpy(dec->d_blob, params, n_params * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
     return bad("decoder weight upload failed");
@@ -1298,6 +1373,13 @@ int pst_decoder_destroy(pst_decoder* dec) {
                   (void*)dec->d_pe_rel, (void*)dec->d_pw, (void*)dec->d_pair, dec->ws})
     if (p) (void)hipFree(p);
   if (dec->blas) (void)rocblas_destroy_handle(dec->blas);
+  for (auto& kv : dec->lt_plans) {
+    if (kv.second.desc) (void)hipblasLtMatmulDescDestroy(kv.second.desc);
+    for (hipblasLtMatrixLayout_t l : {kv.second.a, kv.second.b, kv.second.c})
+      if (l) (void)hipblasLtMatrixLayoutDestroy(l);
+  }
+  if (dec->lt_ws) (void)hipFree(dec->lt_ws);
+  if (dec->lt) (void)hipblasLtDestroy(dec->lt);
   if (dec->stream) (void)hipStreamDestroy(dec->stream);
   delete dec;
   return PST_OK;
