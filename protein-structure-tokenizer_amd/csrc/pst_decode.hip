@@ -468,16 +468,22 @@ __global__ void k_affine_update(float* __restrict__ aff, float* __restrict__ rot
   quat_to_rot(a, R);
 }
 
-// IPA points to the global frame (apply_to_point, quat_affine.py): q [N][12][4][3], kv [N][12][12][3]
+// IPA points to the global frame (apply_to_point, quat_affine.py): q [N][12][4][3], kv [N][12][12][3].
+// Also writes the keys k_ipa_attn's logits read, transposed to [feature][N] so its
+// thread-per-key loads coalesce: kT [192][N] (scalar keys, head-major) and kpT [144][N] (the
+// 4 key points of each head, xyz).
 __global__ void k_ipa_points(const float* __restrict__ qpl /*[N][144]*/, const float* __restrict__ kvpl /*[N][432]*/,
                              const float* __restrict__ aff, const float* __restrict__ rot, float* __restrict__ qpg,
-                             float* __restrict__ kvpg, int N) {
+                             float* __restrict__ kvpg, const float* __restrict__ kvs /*[N][384]*/,
+                             float* __restrict__ kT, float* __restrict__ kpT, int N) {
   const int i = blockIdx.x, t = threadIdx.x;  // 192 threads: 48 q points + 144 kv points
   if (i >= N) return;
+  kT[(int64_t)t * N + i] = kvs[(int64_t)i * 384 + (t / 16) * 32 + t % 16];
   const float* R = rot + i * 9;
   const float* tr = aff + i * 7 + 4;
   float x, y, z;
   float* dst;
+  int kp = -1;  // row of kpT for key points
   if (t < 48) {
     x = qpl[i * 144 + t];
     y = qpl[i * 144 + 48 + t];
@@ -489,8 +495,13 @@ __global__ void k_ipa_points(const float* __restrict__ qpl /*[N][144]*/, const f
     y = kvpl[i * 432 + 144 + p];
     z = kvpl[i * 432 + 288 + p];
     dst = kvpg + ((int64_t)i * 144 + p) * 3;
+    if (p % 12 < 4) kp = ((p / 12) * 4 + p % 12) * 3;
   }
-  for (int r = 0; r < 3; ++r) dst[r] = R[3 * r] * x + R[3 * r + 1] * y + R[3 * r + 2] * z + tr[r];
+  for (int r = 0; r < 3; ++r) {
+    const float v = R[3 * r] * x + R[3 * r + 1] * y + R[3 * r + 2] * z + tr[r];
+    dst[r] = v;
+    if (kp >= 0) kpT[(int64_t)(kp + r) * N + i] = v;
+  }
 }
 
 // Invariant point attention for query residue i (folding.py:69-289): logits over all N residues,
@@ -503,7 +514,9 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
                                                   const float* __restrict__ zln_all /*[pairs][128]*/,
                                                   const float* __restrict__ pw /*[12]*/,
                                                   const float* __restrict__ aff, const float* __restrict__ rot,
-                                                  float* __restrict__ feat /*[N][2112]*/, DecBatch bt) {
+                                                  float* __restrict__ feat /*[N][2112]*/, DecBatch bt,
+                                                  const float* __restrict__ kT_all /*[192][Ntot]*/,
+                                                  const float* __restrict__ kpT_all /*[144][Ntot]*/, int Ntot) {
   __shared__ float att[12][512];
   __shared__ float res_pt[12 * 8 * 3];
   const int64_t ig = blockIdx.x;
@@ -524,9 +537,9 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   for (int e = tid; e < 192; e += 256) qsh[e] = sw * qs[ig * 192 + e];
   for (int e = tid; e < 144; e += 256) qsh[192 + e] = qpg[ig * 144 + e];
   __syncthreads();
+  const float* kT = kT_all + n0;  // column j = key j of this protein
+  const float* kpT = kpT_all + n0;
   for (int j = tid; j < N; j += 256) {
-    const float4* krow = reinterpret_cast<const float4*>(kvs + (int64_t)j * 384);
-    const float4* kprow = reinterpret_cast<const float4*>(kvpg + (int64_t)j * 432);
     const float4* brow = reinterpret_cast<const float4*>(b2d + (int64_t)j * 12);
     float bb[12];
 #pragma unroll
@@ -536,17 +549,12 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
     }
 #pragma unroll 2
     for (int h = 0; h < 12; ++h) {
+      // transposed key rows: lanes read consecutive keys (coalesced)
       float k[16], kp[12];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 v = krow[h * 8 + u];
-        k[4 * u] = v.x; k[4 * u + 1] = v.y; k[4 * u + 2] = v.z; k[4 * u + 3] = v.w;
-      }
+      for (int c = 0; c < 16; ++c) k[c] = kT[(int64_t)(h * 16 + c) * Ntot + j];
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const float4 v = kprow[h * 9 + u];
-        kp[4 * u] = v.x; kp[4 * u + 1] = v.y; kp[4 * u + 2] = v.z; kp[4 * u + 3] = v.w;
-      }
+      for (int c = 0; c < 12; ++c) kp[c] = kpT[(int64_t)(h * 12 + c) * Ntot + j];
       float sc = 0.0f;
 #pragma unroll
       for (int c = 0; c < 16; ++c) sc = __builtin_fmaf(qsh[h * 16 + c], k[c], sc);
@@ -1002,7 +1010,7 @@ struct Scratch {
   float *orig_in, *orig, *res, *ln_a, *ln_b, *q, *k, *v, *gate, *wavg, *tr_h;
   float *left, *right, *P, *h1, *pair0, *catb, *lin_out, *lnz, *z, *zln, *b2d;
   float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
-  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf;
+  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf, *kT, *kpT;
   int64_t *tok_off, *node_off, *pair_off;
   int32_t *tok_prot, *node_prot;
   uint32_t* tokens;
@@ -1032,7 +1040,7 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
                 {(void**)&S->scb, NN * 128 * F},     {(void**)&S->sct, NN * 128 * F},  {(void**)&S->unnorm, NN * 6 * F},
                 {(void**)&S->angles, 8 * NN * 6 * F}, {(void**)&S->traj, 8 * NN * 7 * F},
                 {(void**)&S->atom37, NN * 111 * F},  {(void**)&S->atom14, NN * 42 * F},
-                {(void**)&S->relu_buf, NN * 2112 * F},
+                {(void**)&S->relu_buf, NN * 2112 * F}, {(void**)&S->kT, NN * 192 * F}, {(void**)&S->kpT, NN * 144 * F},
                 {(void**)&S->tok_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->node_off, (NN + 1) * sizeof(int64_t)},
                 {(void**)&S->pair_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->tok_prot, NN * sizeof(int32_t)},
                 {(void**)&S->node_prot, NN * sizeof(int32_t)}, {(void**)&S->tokens, NN * sizeof(uint32_t)}};
@@ -1147,9 +1155,9 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     gemm(st, S.act, 384, W.q_point, S.qpl, 144, Ni, 0);
     gemm(st, S.act, 384, W.kv_point, S.kvpl, 432, Ni, 0);
     hipLaunchKernelGGL(k_ipa_points, dim3((unsigned)N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg,
-                       Ni);
+                       S.kvs, S.kT, S.kpT, Ni);
     hipLaunchKernelGGL(k_ipa_attn, dim3((unsigned)N), dim3(256), 0, st, S.qs, S.kvs, S.qpg, S.kvpg, S.b2d, S.zln,
-                       dec->d_pw, S.aff, S.rot, S.feat, bt);
+                       dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni);
     gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
     layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
     gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
