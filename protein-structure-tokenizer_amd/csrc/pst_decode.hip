@@ -1010,7 +1010,7 @@ struct Scratch {
   float *orig_in, *orig, *res, *ln_a, *ln_b, *q, *k, *v, *gate, *wavg, *tr_h;
   float *left, *right, *P, *h1, *pair0, *catb, *lin_out, *lnz, *z, *zln, *b2d;
   float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
-  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf, *kT, *kpT;
+  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf, *kT, *kpT, *init_relu;
   int64_t *tok_off, *node_off, *pair_off;
   int32_t *tok_prot, *node_prot;
   uint32_t* tokens;
@@ -1041,6 +1041,7 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
                 {(void**)&S->angles, 8 * NN * 6 * F}, {(void**)&S->traj, 8 * NN * 7 * F},
                 {(void**)&S->atom37, NN * 111 * F},  {(void**)&S->atom14, NN * 42 * F},
                 {(void**)&S->relu_buf, NN * 2112 * F}, {(void**)&S->kT, NN * 192 * F}, {(void**)&S->kpT, NN * 144 * F},
+                {(void**)&S->init_relu, NN * 128 * F},
                 {(void**)&S->tok_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->node_off, (NN + 1) * sizeof(int64_t)},
                 {(void**)&S->pair_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->tok_prot, NN * sizeof(int32_t)},
                 {(void**)&S->node_prot, NN * sizeof(int32_t)}, {(void**)&S->tokens, NN * sizeof(uint32_t)}};
@@ -1149,6 +1150,9 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
                        0.577350269189626f);
   }
   hipLaunchKernelGGL(k_affine_init, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, Ni);
+  // relu(init_act) feeds the angle resnet of every iteration: once, not 8 copies
+  hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.init_act, 128, S.init_relu,
+                     (int64_t)Ni, 128);
   for (int it = 0; it < 8; ++it) {
     gemm(st, S.act, 384, W.q_scalar, S.qs, 192, Ni, 0);
     gemm(st, S.act, 384, W.kv_scalar, S.kvs, 384, Ni, 0);
@@ -1169,11 +1173,13 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     // MultiRigidSidechain: (0 + Lin(relu(act))) + Lin(relu(initial_act)), 2 residual blocks, angles
     hipLaunchKernelGGL(k_zero, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.sca, N * 128);
     gemm(st, S.act, 384, W.sc_in, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
-    gemm(st, S.init_act, 128, W.sc_in1, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
-    gemm(st, S.sca, 128, W.rb1, S.scb, 128, Ni, F_RELU_IN);
-    gemm(st, S.scb, 128, W.rb2, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
-    gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, Ni, F_RELU_IN);
-    gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
+    gemm(st, S.init_relu, 128, W.sc_in1, S.sca, 128, Ni, F_ACCUM);
+    // scb is only ever read through a ReLU: apply it in the producing GEMM's epilogue instead of
+    // as a copy before the consumer (same values)
+    gemm(st, S.sca, 128, W.rb1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
+    gemm(st, S.scb, 128, W.rb2, S.sca, 128, Ni, F_ACCUM);
+    gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
+    gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, Ni, F_ACCUM);
     gemm(st, S.sca, 128, W.angles, S.unnorm, 6, Ni, F_RELU_IN);
     const bool last = it == 7;
     hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.unnorm,
