@@ -128,3 +128,22 @@ def test_fused_pair_kernel_matches_library_path(monkeypatch):
     assert np.max(np.abs(z_fused - z_ref)) / np.max(np.abs(z_ref)) < 2e-5
     for a, b in zip(fused, ref):
         assert np.max(np.abs(a - b)) < 1e-3
+
+
+def test_gemm_backends_agree(monkeypatch):
+    """The per-node GEMMs on hipBLASLt with the fused bias/ReLU epilogue (default), on rocBLAS +
+    the epilogue kernel (PST_DECODE_NO_LT=1) and on the in-tree LDS-tiled kernel
+    (PST_DECODE_NO_BLAS=1) give the same structures to float32 reordering noise."""
+    from pst_amd._native import Decoder
+    rng = np.random.default_rng(17)
+    toks = [rng.integers(0, 4096, n) for n in (64, 23, 130)]
+    dec = Decoder(0, 4096, 1, P.pack_decoder(P.random_full_params(6, 13), 6))
+    base = dec.decode(toks)
+    for env in ("PST_DECODE_NO_LT", "PST_DECODE_NO_BLAS"):
+        monkeypatch.setenv(env, "1")
+        other = dec.decode(toks)
+        monkeypatch.delenv(env)
+        for a, b in zip(base, other):
+            assert np.all(np.isfinite(b))
+            assert np.max(np.abs(a - b)) < 1e-3, env
+    dec.close()
