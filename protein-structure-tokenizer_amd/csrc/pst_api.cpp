@@ -44,6 +44,14 @@ constexpr double DOWN_COOP_SIMD_FRACTION = 0.375;
 // tasks per SIMD, k_mpnn_node (one wave) above.
 constexpr double NODE_COOP_SIMD_FRACTION = 0.375;
 
+// Schedule thresholds from the environment, read once per context: -2 = not read yet, -1 = unset
+// (use the cost model), >= 0 = the override.
+void env_threshold(int64_t& v, const char* name) {
+  if (v != -2) return;
+  const char* e = getenv(name);
+  v = e ? std::max<int64_t>(0, atoll(e)) : -1;
+}
+
 thread_local std::string g_create_error;
 
 
@@ -495,15 +503,9 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   // layer split: edge blocks spread over ~4096 waves, messages through HBM, ordered sums in
   // k_seg_sum, node update; bit-identical results.
   const int64_t n_tasks = Rpad / 32;
-  if (ctx->split_tasks == -2) {
-    const char* e = getenv("PST_SPLIT_TASKS");
-    ctx->split_tasks = e ? std::max<int64_t>(0, atoll(e)) : -1;
-  }
+  env_threshold(ctx->split_tasks, "PST_SPLIT_TASKS");
   const bool split = ctx->split_tasks >= 0 ? n_tasks <= ctx->split_tasks : use_split_schedule(n_tasks, ctx->n_simds);
-  if (ctx->node_coop == -2) {
-    const char* e = getenv("PST_NODE_COOP");
-    ctx->node_coop = e ? std::max<int64_t>(0, atoll(e)) : -1;
-  }
+  env_threshold(ctx->node_coop, "PST_NODE_COOP");
   const bool node_coop =
       split && n_tasks <= (ctx->node_coop >= 0 ? ctx->node_coop : (int64_t)(NODE_COOP_SIMD_FRACTION * ctx->n_simds));
   float* msg_rows = nullptr;
@@ -613,10 +615,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   d.bounded_out = w.bounded;
   d.quant_out = w.quant;
   d.pre_proj_out = w.pre_proj;
-  if (ctx->down_coop == -2) {
-    const char* e = getenv("PST_DOWN_COOP");
-    ctx->down_coop = e ? std::max<int64_t>(0, atoll(e)) : -1;
-  }
+  env_threshold(ctx->down_coop, "PST_DOWN_COOP");
   const int64_t coop_max = ctx->down_coop >= 0 ? ctx->down_coop : (int64_t)(DOWN_COOP_SIMD_FRACTION * ctx->n_simds);
   if (d.n_tiles > 0) pst::launch_down(ctx->df, d, d.n_tiles <= coop_max, st);
   mark(ctx, 6);
