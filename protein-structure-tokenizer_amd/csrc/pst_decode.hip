@@ -589,60 +589,69 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   }
   __syncthreads();
   float* f = feat + ig * 2112;
-  // scalar values (192) and global value points (288); the key loops are unrolled 8-wide with
-  // the 8 loads issued ahead of the (in-order) fmaf chain, so a thread keeps 8 loads in flight
-  for (int o = tid; o < 192 + 288; o += 256) {
-    int h, q = 0;
-    const float* src;
-    int64_t stride;
-    if (o < 192) {
-      h = o / 16;
-      src = kvs + h * 32 + 16 + o % 16;
-      stride = 384;
-    } else {
-      q = o - 192;
-      h = q / 24;
-      src = kvpg + (h * 12 + 4 + (q / 3) % 8) * 3 + q % 3;
-      stride = 432;
-    }
-    const float* arow = att[h];
-    float acc = 0.0f;
-    int j = 0;
-    for (; j + 8 <= N; j += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(j + u) * stride];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc = __builtin_fmaf(arow[j + u], v[u], acc);
-    }
-    for (; j < N; ++j) acc = __builtin_fmaf(arow[j], src[(int64_t)j * stride], acc);
-    if (o < 192)
-      f[o] = acc;
-    else
-      res_pt[q] = acc;
-  }
-  // attention over the pair representation: thread → channel c, heads hg, hg+2, ...
+  // One pass over the keys feeds all 2016 weighted sums of this query: per thread the pair
+  // attention of channel c for heads hg, hg+2, ... (6 sums) and value outputs o = tid and
+  // tid + 256 (scalar values 0..191, global value points 192..479). Each sum is its own in-order
+  // fmaf chain over j; loads run 8 keys ahead.
   {
     const int c = tid & 127, hg = tid >> 7;
-    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const float* zr = zln + c;
+    const float* vsrc[2];
+    int64_t vstride[2];
+    int vh[2];
+    bool vok[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int o = tid + 256 * m;
+      vok[m] = o < 192 + 288;
+      if (o < 192) {
+        vh[m] = o / 16;
+        vsrc[m] = kvs + vh[m] * 32 + 16 + o % 16;
+        vstride[m] = 384;
+      } else {
+        const int q = vok[m] ? o - 192 : 0;
+        vh[m] = q / 24;
+        vsrc[m] = kvpg + (vh[m] * 12 + 4 + (q / 3) % 8) * 3 + q % 3;
+        vstride[m] = 432;
+      }
+    }
+    float pacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float vacc[2] = {0.f, 0.f};
     int j = 0;
     for (; j + 8 <= N; j += 8) {
-      float zv[8];
+      float zv[8], v0[8], v1[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) zv[u] = zr[(int64_t)(j + u) * 128];
+      for (int u = 0; u < 8; ++u) {
+        zv[u] = zr[(int64_t)(j + u) * 128];
+        v0[u] = vsrc[0][(int64_t)(j + u) * vstride[0]];
+        v1[u] = vok[1] ? vsrc[1][(int64_t)(j + u) * vstride[1]] : 0.0f;
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < 8; ++u) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) acc[k] = __builtin_fmaf(att[hg + 2 * k][j + u], zv[u], acc[k]);
+        for (int k = 0; k < 6; ++k) pacc[k] = __builtin_fmaf(att[hg + 2 * k][j + u], zv[u], pacc[k]);
+        vacc[0] = __builtin_fmaf(att[vh[0]][j + u], v0[u], vacc[0]);
+        vacc[1] = __builtin_fmaf(att[vh[1]][j + u], v1[u], vacc[1]);
+      }
     }
     for (; j < N; ++j) {
       const float zv = zr[(int64_t)j * 128];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) acc[k] = __builtin_fmaf(att[hg + 2 * k][j], zv, acc[k]);
+      for (int k = 0; k < 6; ++k) pacc[k] = __builtin_fmaf(att[hg + 2 * k][j], zv, pacc[k]);
+      vacc[0] = __builtin_fmaf(att[vh[0]][j], vsrc[0][(int64_t)j * vstride[0]], vacc[0]);
+      if (vok[1]) vacc[1] = __builtin_fmaf(att[vh[1]][j], vsrc[1][(int64_t)j * vstride[1]], vacc[1]);
     }
 #pragma unroll
-    for (int u = 0; u < 6; ++u) f[576 + (hg + 2 * u) * 128 + c] = acc[u];
+    for (int u = 0; u < 6; ++u) f[576 + (hg + 2 * u) * 128 + c] = pacc[u];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int o = tid + 256 * m;
+      if (!vok[m]) continue;
+      if (o < 192)
+        f[o] = vacc[m];
+      else
+        res_pt[o - 192] = vacc[m];
+    }
   }
   __syncthreads();
   // global → local frame of i (invert_point) and norms
