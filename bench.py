@@ -176,7 +176,9 @@ def main():
     roofline = {
         "kernel": "k_mpnn<1> (edge MLP L1 + message MLP L2 + node FFN, fused)",
         "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+        "traffic": traffic["bytes_per_launch"] if traffic else None,  # HBM bytes per launch (PMC)
+        "traffic_detail": traffic,
         "note": "achieved/frac count SURVEY 8d algorithmic FLOPs; the kernel executes "
                 f"{MPNN1_EXEC_FLOP_PER_RES / MPNN1_ALG_FLOP_PER_RES:.3f}x of them (node-projection split, "
                 "message last layer after the segment sum; DESIGN.md 5): executed_tflops/peak = frac_executed",
