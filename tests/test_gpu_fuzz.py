@@ -1,0 +1,62 @@
+"""Randomised GPU parity sweep: ragged batches of random sizes with randomly missing atoms and
+backbone (filtered residues, short-protein branch), over every codebook / downsampling pair the
+reference ships, against the CPU oracle — token ids exact, bounded codes and pre-projection
+embeddings bitwise. Seeded, so a failure reproduces."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pst_amd import params as P
+from pst_amd import synthetic
+from pst_amd.config import LEVELS
+
+pytestmark = pytest.mark.gpu
+
+_TK = {}
+
+
+def _tokenizer(cb, df):
+    if (cb, df) not in _TK:
+        from pst_amd._native import Tokenizer
+        _TK[(cb, df)] = Tokenizer(0, cb, df, P.random_blob(len(LEVELS[cb]), 4242))
+    return _TK[(cb, df)]
+
+
+def _damaged(n, seed, rng):
+    s = synthetic.synthetic_protein(n, seed)
+    gt = s.atom37_gt_exists.copy()
+    gt &= rng.random(gt.shape) > 0.03  # scattered missing atoms (centroids change)
+    drop = rng.random(n) < 0.04  # residues losing a backbone atom are filtered out
+    gt[drop, rng.integers(0, 3, int(drop.sum()))] = False
+    return s._replace(atom37_gt_exists=gt)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_batches_match_oracle(seed):
+    from pst_amd._native import pack_samples
+    rng = np.random.default_rng(1000 + seed)
+    cb = [4096, 64000, 432, 1728][seed % 4]
+    df = [1, 2, 4][seed % 3]
+    sizes = rng.integers(52, 513, int(rng.integers(1, 6))).tolist()
+    if seed % 2:
+        sizes.append(int(rng.integers(50, 60)))  # near the 50-residue gate: short-protein branch
+    samples = [_damaged(n, 31 * seed + i, rng) for i, n in enumerate(sizes)]
+    tk = _tokenizer(cb, df)
+    pos, flags, off = pack_samples(samples)
+    try:
+        tok, nt, nn = tk.tokenize_packed(pos, flags, off)
+    except NotImplementedError:
+        pytest.skip("a damaged protein fell under the 50-residue gate")
+    R = int(off[-1])
+    aux = tk.aux(R)
+    blob = P.random_blob(len(LEVELS[cb]), 4242)
+    for b, s in enumerate(samples):
+        o = O.tokenize(blob, LEVELS[cb], df, s.atom37_positions, s.atom_flags())
+        n = o["graph"]["n"]
+        assert nn[b] == n
+        T = n // df
+        assert nt[b] == T
+        base = int(off[b])
+        assert np.array_equal(tok[base: base + T], o["tokens"]), (seed, b)
+        assert np.array_equal(aux["bounded"][base: base + T].view(np.uint32), o["b"].view(np.uint32))
+        assert np.array_equal(aux["pre_proj"][base: base + T].view(np.uint32), o["pre_proj"].view(np.uint32))
