@@ -26,7 +26,7 @@ constexpr int KNN = 50;
 // k = ceil(tasks / SIMDs): about k·SIMDs task-units for k >= 2 and 1.1·SIMDs for k = 1 (one
 // wave per SIMD runs alone). The split schedule costs about 1.1 units per task (message rows
 // through HBM). Split wins below ~1 000 tasks and in the half-empty rounds above.
-constexpr double SPLIT_COST_PER_TASK = 1.1;
+constexpr double SPLIT_COST_PER_TASK = 1.05;  // one edge block per wave (re-measured, tools/policy_check.sh)
 constexpr double FUSED_SINGLE_ROUND = 1.1;
 bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
   const int64_t k = (n_tasks + n_simds - 1) / n_simds;
@@ -43,6 +43,11 @@ constexpr double DOWN_COOP_SIMD_FRACTION = 0.375;
 // Split-schedule node update: k_mpnn_node_coop (four waves per 32 receivers) up to this many
 // tasks per SIMD, k_mpnn_node (one wave) above.
 constexpr double NODE_COOP_SIMD_FRACTION = 0.375;
+// Split schedule: one 32-edge block per wave by default. Waves run in rounds of (2 per SIMD)
+// slots, so b blocks per wave cost ceil(ceil(B/b)/slots)·b block times — minimal at b = 1
+// (measured: 32 proteins 2.75 -> 2.41 ms, CASP14 1.82 -> 1.78 ms vs ~4096 waves of 2-4 blocks;
+// tools/edge_waves_sizes.sh). PST_EDGE_WAVES=n targets about n waves instead.
+constexpr int64_t SPLIT_EDGE_WAVES = 0;
 
 // Schedule thresholds from the environment, read once per context: -2 = not read yet, -1 = unset
 // (use the cost model), >= 0 = the override.
@@ -201,6 +206,7 @@ struct pst_ctx {
   size_t msg_bytes = 0;
   int64_t split_tasks = -2;  // PST_SPLIT_TASKS: split iff n_tasks <= this; -1 = cost model; -2 = not read yet
   int64_t n_simds = 1024;    // 4 x compute units of the device
+  int64_t edge_waves = -2;   // PST_EDGE_WAVES: split-schedule edge waves target; -1 = SPLIT_EDGE_WAVES
   int64_t node_coop = -2;    // PST_NODE_COOP: k_mpnn_node_coop iff split and n_tasks <= this; -1 = default
   int64_t down_coop = -2;    // PST_DOWN_COOP: k_down_coop iff n_tiles <= this; -1 = default; -2 = not read yet
   std::vector<int64_t> h_offsets;
@@ -524,7 +530,9 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
       ctx->msg_bytes = need;
     }
     msg_rows = ctx->msg;
-    bpw = (int32_t)std::max<int64_t>(1, (n_tasks * 50 + 4095) / 4096);
+    env_threshold(ctx->edge_waves, "PST_EDGE_WAVES");
+    const int64_t target = ctx->edge_waves > 0 ? ctx->edge_waves : SPLIT_EDGE_WAVES;
+    bpw = target > 0 ? (int32_t)std::max<int64_t>(1, (n_tasks * 50 + target - 1) / target) : 1;
   }
   float* hbuf[4] = {nullptr, w.h0, w.h1, w.h0};
   float* ebuf[3] = {w.e0, w.e1, nullptr};
