@@ -506,7 +506,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     return pst::MlpW{F4(o.w0), A + o.b0, F4(o.w1), A + o.b1, F4(o.w2), A + o.b2, F4(o.bf1), F4(o.bf2)};
   };
   // Batches whose 32-receiver tasks leave fused rounds half empty (use_split_schedule) run each
-  // layer split: edge blocks spread over ~4096 waves, messages through HBM, ordered sums in
+  // layer split: one edge block per wave, messages through HBM, ordered sums in
   // k_seg_sum, node update; bit-identical results.
   const int64_t n_tasks = Rpad / 32;
   env_threshold(ctx->split_tasks, "PST_SPLIT_TASKS");
