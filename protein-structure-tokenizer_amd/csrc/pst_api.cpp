@@ -586,8 +586,13 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     mark(ctx, 3 + l);
     if (ctx->dbg[l]) HIPCHK(hipMemcpyAsync(ctx->dbg[l], m.h_out, sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
   }
-  // downsampler's original track works on a copy of h3 (h3 stays available to pst_debug_fetch)
-  HIPCHK(hipMemcpyAsync(w.h1, hbuf[3], sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
+  // k_down updates the original track in place, so it works on a copy of h3 (h3 stays available
+  // to pst_debug_fetch); k_down_coop (df 1, small batches) keeps the track in registers and
+  // reads h3 directly
+  env_threshold(ctx->down_coop, "PST_DOWN_COOP");
+  const int64_t coop_max = ctx->down_coop >= 0 ? ctx->down_coop : (int64_t)(DOWN_COOP_SIMD_FRACTION * ctx->n_simds);
+  const bool down_coop = ctx->df == 1 && (int64_t)tp.size() <= coop_max;
+  if (!down_coop) HIPCHK(hipMemcpyAsync(w.h1, hbuf[3], sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
   pst::DownArgs d{};
   d.n_tiles = (int32_t)tp.size();
   d.tile_prot = w.tile_prot;
@@ -595,7 +600,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   d.offsets = w.offsets;
   d.n_nodes = d_nnodes;
   d.RPE = ctx->d_RPE;
-  d.o_buf = w.h1;
+  d.o_buf = down_coop ? hbuf[3] : w.h1;
   d.r_buf = w.r_buf;
   d.v_buf = w.v_buf;
   for (int b = 0; b < 3; ++b) {
@@ -623,9 +628,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   d.bounded_out = w.bounded;
   d.quant_out = w.quant;
   d.pre_proj_out = w.pre_proj;
-  env_threshold(ctx->down_coop, "PST_DOWN_COOP");
-  const int64_t coop_max = ctx->down_coop >= 0 ? ctx->down_coop : (int64_t)(DOWN_COOP_SIMD_FRACTION * ctx->n_simds);
-  if (d.n_tiles > 0) pst::launch_down(ctx->df, d, d.n_tiles <= coop_max, st);
+  if (d.n_tiles > 0) pst::launch_down(ctx->df, d, down_coop, st);
   mark(ctx, 6);
   HIPCHK(hipGetLastError());
   ctx->last_R = R;
