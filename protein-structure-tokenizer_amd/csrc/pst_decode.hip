@@ -475,25 +475,25 @@ __global__ void k_affine_update(float* __restrict__ aff, float* __restrict__ rot
 __global__ void k_ipa_points(const float* __restrict__ qpl /*[N][144]*/, const float* __restrict__ kvpl /*[N][432]*/,
                              const float* __restrict__ aff, const float* __restrict__ rot, float* __restrict__ qpg,
                              float* __restrict__ kvpg, const float* __restrict__ kvs /*[N][384]*/,
-                             float* __restrict__ kT, float* __restrict__ kpT, int N) {
+                             float* __restrict__ kT, float* __restrict__ kpT, int N, int ld) {
   const int i = blockIdx.x, t = threadIdx.x;  // 192 threads: 48 q points + 144 kv points
   if (i >= N) return;
-  kT[(int64_t)t * N + i] = kvs[(int64_t)i * 384 + (t / 16) * 32 + t % 16];
+  kT[(int64_t)t * N + i] = kvs[(int64_t)i * ld + (t / 16) * 32 + t % 16];
   const float* R = rot + i * 9;
   const float* tr = aff + i * 7 + 4;
   float x, y, z;
   float* dst;
   int kp = -1;  // row of kpT for key points
   if (t < 48) {
-    x = qpl[i * 144 + t];
-    y = qpl[i * 144 + 48 + t];
-    z = qpl[i * 144 + 96 + t];
+    x = qpl[(int64_t)i * ld + t];
+    y = qpl[(int64_t)i * ld + 48 + t];
+    z = qpl[(int64_t)i * ld + 96 + t];
     dst = qpg + ((int64_t)i * 48 + t) * 3;
   } else {
     const int p = t - 48;
-    x = kvpl[i * 432 + p];
-    y = kvpl[i * 432 + 144 + p];
-    z = kvpl[i * 432 + 288 + p];
+    x = kvpl[(int64_t)i * ld + p];
+    y = kvpl[(int64_t)i * ld + 144 + p];
+    z = kvpl[(int64_t)i * ld + 288 + p];
     dst = kvpg + ((int64_t)i * 144 + p) * 3;
     if (p % 12 < 4) kp = ((p / 12) * 4 + p % 12) * 3;
   }
@@ -516,7 +516,8 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
                                                   const float* __restrict__ aff, const float* __restrict__ rot,
                                                   float* __restrict__ feat /*[N][2112]*/, DecBatch bt,
                                                   const float* __restrict__ kT_all /*[192][Ntot]*/,
-                                                  const float* __restrict__ kpT_all /*[144][Ntot]*/, int Ntot) {
+                                                  const float* __restrict__ kpT_all /*[144][Ntot]*/, int Ntot,
+                                                  int ld /*row stride of qs and kvs*/) {
   __shared__ float att[12][512];
   __shared__ float res_pt[12 * 8 * 3];
   const int64_t ig = blockIdx.x;
@@ -526,7 +527,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   const int N = (int)(bt.node_off[bprot + 1] - n0);
   const int il = (int)(ig - n0);
   // protein-local views: rows j of kvs/kvpg, pair rows (il, j) of b2d/zln
-  const float* kvs = kvs_all + n0 * 384;
+  const float* kvs = kvs_all + n0 * ld;
   const float* kvpg = kvpg_all + n0 * 432;
   const float* b2d = b2d_all + (bt.pair_off[bprot] + (int64_t)il * N) * 12;
   const float* zln = zln_all + (bt.pair_off[bprot] + (int64_t)il * N) * 128;
@@ -534,7 +535,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   // logits: one key per thread, all 12 heads, from 16-byte loads of the key's rows; the query
   // (scaled scalar part and global points) is shared through LDS
   __shared__ float qsh[192 + 144];
-  for (int e = tid; e < 192; e += 256) qsh[e] = sw * qs[ig * 192 + e];
+  for (int e = tid; e < 192; e += 256) qsh[e] = sw * qs[ig * ld + e];
   for (int e = tid; e < 144; e += 256) qsh[192 + e] = qpg[ig * 144 + e];
   __syncthreads();
   const float* kT = kT_all + n0;  // column j = key j of this protein
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
       if (o < 192) {
         vh[m] = o / 16;
         vsrc[m] = kvs + vh[m] * 32 + 16 + o % 16;
-        vstride[m] = 384;
+        vstride[m] = ld;
       } else {
         const int q = vok[m] ? o - 192 : 0;
         vh[m] = q / 24;
@@ -800,6 +801,8 @@ struct pst_decoder {
     size_t ws = 0;
     bool ok = false;
   };
+  float* d_ipa_w = nullptr;  // [384][1152]: q_scalar | kv_scalar | q_point | kv_point weights
+  float* d_ipa_b = nullptr;  // [1152] their biases
   hipblasLtHandle_t lt = nullptr;
   void* lt_ws = nullptr;
   size_t lt_ws_bytes = 0;
@@ -1019,7 +1022,7 @@ struct Scratch {
   float *orig_in, *orig, *res, *ln_a, *ln_b, *q, *k, *v, *gate, *wavg, *tr_h;
   float *left, *right, *P, *h1, *pair0, *catb, *lin_out, *lnz, *z, *zln, *b2d;
   float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
-  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf, *kT, *kpT, *init_relu;
+  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf, *kT, *kpT, *init_relu, *ipa_in;
   int64_t *tok_off, *node_off, *pair_off;
   int32_t *tok_prot, *node_prot;
   uint32_t* tokens;
@@ -1042,8 +1045,8 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
                 {(void**)&S->b2d, NP * 12 * F},      {(void**)&S->single_ln, NN * 128 * F},
                 {(void**)&S->act, NN * 384 * F},     {(void**)&S->init_act, NN * 128 * F},
                 {(void**)&S->act_ln, NN * 384 * F},  {(void**)&S->tmp384a, NN * 384 * F},
-                {(void**)&S->tmp384b, NN * 384 * F}, {(void**)&S->qs, NN * 192 * F},   {(void**)&S->kvs, NN * 384 * F},
-                {(void**)&S->qpl, NN * 144 * F},     {(void**)&S->kvpl, NN * 432 * F}, {(void**)&S->qpg, NN * 144 * F},
+                {(void**)&S->tmp384b, NN * 384 * F}, {(void**)&S->ipa_in, NN * 1152 * F},
+                {(void**)&S->qpg, NN * 144 * F},
                 {(void**)&S->kvpg, NN * 432 * F},    {(void**)&S->feat, NN * 2112 * F}, {(void**)&S->upd, NN * 6 * F},
                 {(void**)&S->aff, NN * 7 * F},       {(void**)&S->rot, NN * 9 * F},    {(void**)&S->sca, NN * 128 * F},
                 {(void**)&S->scb, NN * 128 * F},     {(void**)&S->sct, NN * 128 * F},  {(void**)&S->unnorm, NN * 6 * F},
@@ -1066,6 +1069,10 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
     *it.p = p;
     p += (it.bytes + 255) / 256 * 256;
   }
+  S->qs = S->ipa_in;  // column blocks of the fused projection output
+  S->kvs = S->ipa_in + 192;
+  S->qpl = S->ipa_in + 576;
+  S->kvpl = S->ipa_in + 720;
   return PST_OK;
 }
 
@@ -1163,14 +1170,13 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.init_act, 128, S.init_relu,
                      (int64_t)Ni, 128);
   for (int it = 0; it < 8; ++it) {
-    gemm(st, S.act, 384, W.q_scalar, S.qs, 192, Ni, 0);
-    gemm(st, S.act, 384, W.kv_scalar, S.kvs, 384, Ni, 0);
-    gemm(st, S.act, 384, W.q_point, S.qpl, 144, Ni, 0);
-    gemm(st, S.act, 384, W.kv_point, S.kvpl, 432, Ni, 0);
+    // the four IPA input projections as one 384 -> 1152 GEMM: [q_scalar | kv_scalar | q_point |
+    // kv_point] columns of ipa_in (row stride 1152)
+    gemm_raw(st, S.act, 384, dec->d_ipa_w, 384, 1152, dec->d_ipa_b, S.ipa_in, 1152, Ni, 0);
     hipLaunchKernelGGL(k_ipa_points, dim3((unsigned)N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg,
-                       S.kvs, S.kT, S.kpT, Ni);
+                       S.kvs, S.kT, S.kpT, Ni, 1152);
     hipLaunchKernelGGL(k_ipa_attn, dim3((unsigned)N), dim3(256), 0, st, S.qs, S.kvs, S.qpg, S.kvpg, S.b2d, S.zln,
-                       dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni);
+                       dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152);
     gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
     layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
     gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
@@ -1359,6 +1365,22 @@ int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* 
       hipMemcpy(dec->d_blob, params, n_params * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
     return bad("decoder weight upload failed");
   walk_decoder(dec->d_blob, D, &dec->W);
+  {
+    if (hipMalloc(&dec->d_ipa_w, 384 * 1152 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&dec->d_ipa_b, 1152 * sizeof(float)) != hipSuccess)
+      return bad("IPA projection buffer allocation failed");
+    int col = 0;
+    for (const Lin* L : {&dec->W.q_scalar, &dec->W.kv_scalar, &dec->W.q_point, &dec->W.kv_point}) {
+      if (L->in != 384 ||
+          hipMemcpy2D(dec->d_ipa_w + col, 1152 * sizeof(float), L->w, L->out * sizeof(float), L->out * sizeof(float),
+                      384, hipMemcpyDeviceToDevice) != hipSuccess ||
+          (L->b ? hipMemcpy(dec->d_ipa_b + col, L->b, L->out * sizeof(float), hipMemcpyDeviceToDevice)
+                : hipMemset(dec->d_ipa_b + col, 0, L->out * sizeof(float))) != hipSuccess)
+        return bad("IPA projection weight packing failed");
+      col += L->out;
+    }
+    if (col != 1152) return bad("IPA projection widths do not add up to 1152");
+  }
   // host-side constants: PE tables, levels, IPA point weights
   auto up = [&](float** d, const std::vector<float>& h) {
     return hipMalloc(d, h.size() * sizeof(float)) == hipSuccess &&
@@ -1393,7 +1415,8 @@ int pst_decoder_destroy(pst_decoder* dec) {
   (void)hipSetDevice(dec->device);
   if (dec->stream) (void)hipStreamSynchronize(dec->stream);
   for (void* p : {(void*)dec->d_blob, (void*)dec->d_levels, (void*)dec->d_pe_node, (void*)dec->d_pe_tok,
-                  (void*)dec->d_pe_rel, (void*)dec->d_pw, (void*)dec->d_pair, dec->ws})
+                  (void*)dec->d_pe_rel, (void*)dec->d_pw, (void*)dec->d_pair, dec->ws, (void*)dec->d_ipa_w,
+                  (void*)dec->d_ipa_b})
     if (p) (void)hipFree(p);
   if (dec->blas) (void)rocblas_destroy_handle(dec->blas);
   for (auto& kv : dec->lt_plans) {
