@@ -8,7 +8,7 @@
  *                    (scripts/inference_runner.py:180-191, 237-248): one context per GPU holding
  *                    the encoder-half parameters and precomputed input-independent tables.
  *   pst_tokenize     make_graph_from_pdb → preprocess_sample (structure_tokenizer/data/
- *                    preprocessing.py:42-283; graph build: utils/protein_utils.py:636-749,
+ *                    preprocessing.py:42-283; graph build: utils/protein_utils.py:325-438,
  *                    model/quat_affine.py:406-522) + the pmap'd Vq3D.encode_and_quantize
  *                    (model/model.py:453-479) + tokens D2H (scripts/inference_runner.py:303-306).
  *                    Host buffers in, host token ids out (synchronous).

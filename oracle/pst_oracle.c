@@ -7,7 +7,7 @@
  *   - preprocess_sample's graph (structure_tokenizer/data/preprocessing.py:42-283):
  *     backbone filter (protein_structure_sample.py:64-70), frames
  *     (model/quat_affine.py:406-522), centroids / cdist / k-NN / RBF / p,q,k,t features
- *     (utils/protein_utils.py:568-592, 636-749) and the padding semantics of
+ *     (utils/protein_utils.py:257-281 RBFs, 325-438 graph) and the padding semantics of
  *     preprocessing.py:191-271 (incl. the < k residue branch), in float64 with the numpy
  *     operation order, rounded once to float32 (JAX's device transfer);
  *   - Vq3D.encode_and_quantize (model/model.py:357-479): positional encodings
@@ -319,7 +319,7 @@ static int cmp_dk(const void* a, const void* b) {
  * ((+0 + p0) + p2) + p1 (measured against numpy 2.2 in the build container; tests pin it) */
 static double dot3(const double* b, const double* x) { return ((0.0 + b[0] * x[0]) + b[2] * x[2]) + b[1] * x[1]; }
 
-/* 27 edge features of edge (receiver r, sender s), protein_utils.py:568-592, 715-745 */
+/* 27 edge features of edge (receiver r, sender s), protein_utils.py:257-281 (RBF), 409-434 (p,q,k,t) */
 static void edge_features(int r, int s, double dist, const double* ca, const frame_t* fr, float* out) {
   double d2 = dist * dist;
   double ls = 1.0;

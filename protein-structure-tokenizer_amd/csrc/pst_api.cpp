@@ -48,6 +48,12 @@ constexpr double NODE_COOP_SIMD_FRACTION = 0.375;
 // (measured: 32 proteins 2.75 -> 2.41 ms, CASP14 1.82 -> 1.78 ms vs ~4096 waves of 2-4 blocks;
 // tools/edge_waves_sizes.sh). PST_EDGE_WAVES=n targets about n waves instead.
 constexpr int64_t SPLIT_EDGE_WAVES = 0;
+// Host-buffer calls (pst_tokenize) pipeline the atom37 H2D (≈925 B per residue, ~60 GB/s) with the
+// compute (~5 M residues/s) in up to H2D_MAX_CHUNKS protein chunks once the batch has at least
+// H2D_MIN_CHUNK_TASKS 32-residue tasks per chunk: each chunk then still fills the GPU for >= 2
+// fused rounds, and only the first chunk's copy is exposed.
+constexpr int H2D_MAX_CHUNKS = 8;
+constexpr int64_t H2D_MIN_CHUNK_TASKS = 4096;
 
 // Schedule thresholds from the environment, read once per context: -2 = not read yet, -1 = unset
 // (use the cost model), >= 0 = the override.
@@ -210,6 +216,12 @@ struct pst_ctx {
   int64_t node_coop = -2;    // PST_NODE_COOP: k_mpnn_node_coop iff split and n_tasks <= this; -1 = default
   int64_t down_coop = -2;    // PST_DOWN_COOP: k_down_coop iff n_tiles <= this; -1 = default; -2 = not read yet
   std::vector<int64_t> h_offsets;
+  // pst_tokenize's H2D pipeline: proteins copied in chunks on copy_stream, chunk k+1's copy
+  // overlapping chunk k's compute on `stream` (H2D_MAX_CHUNKS events)
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t copy_ev[8] = {};
+  int64_t h2d_chunks = -2;  // PST_H2D_CHUNKS: force the chunk count (1 = no pipeline); -1 = policy
+  bool chunked_last = false; // last call was pipelined: per-layer debug intermediates hold its last chunk only
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
   bool timing = false;
@@ -462,15 +474,11 @@ int validate(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot) {
   return PST_OK;
 }
 
-int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t* offsets, int32_t n_prot,
-        uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes, bool graph_only = false) {
-  const int64_t R = offsets[n_prot];
-  int rc = ensure_workspace(ctx, R, n_prot);
-  if (rc) return rc;
+// Per-protein token tiles of 32 (upper bound from the raw residue counts) → w.tile_prot/tile_t0,
+// and the batch offsets → w.offsets (stream-ordered uploads)
+int upload_batch_meta(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot, int32_t* n_tiles) {
   auto& w = ctx->w;
-  const int64_t Rpad = (R + 127) / 128 * 128;
   hipStream_t st = ctx->stream;
-  // per-protein token tiles of 32 (upper bound from the raw residue count)
   std::vector<int32_t> tp, tt;
   for (int b = 0; b < n_prot; ++b) {
     int64_t Tmax = (offsets[b + 1] - offsets[b]) / ctx->df;
@@ -481,8 +489,29 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   }
   ctx->h_offsets.assign(offsets, offsets + n_prot + 1);
   HIPCHK(hipMemcpyAsync(w.offsets, ctx->h_offsets.data(), sizeof(int64_t) * (n_prot + 1), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(w.tile_prot, tp.data(), sizeof(int32_t) * tp.size(), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(w.tile_t0, tt.data(), sizeof(int32_t) * tt.size(), hipMemcpyHostToDevice, st));
+  if (!tp.empty()) {
+    HIPCHK(hipMemcpyAsync(w.tile_prot, tp.data(), sizeof(int32_t) * tp.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(w.tile_t0, tt.data(), sizeof(int32_t) * tt.size(), hipMemcpyHostToDevice, st));
+  }
+  *n_tiles = (int32_t)tp.size();
+  return PST_OK;
+}
+
+// One batch (or one chunk of a pipelined batch) through graph → encoder → downsampler/FSQ on
+// ctx->stream. `out_row0`: raw residue row of offsets[0] in the caller's batch, where the
+// raw-layout aux outputs (bounded, quantize, pre_proj) of this batch go.
+int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t* offsets, int32_t n_prot,
+        uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes, bool graph_only = false, int64_t out_row0 = 0) {
+  const int64_t R = offsets[n_prot];
+  int rc = ensure_workspace(ctx, R, n_prot);
+  if (rc) return rc;
+  auto& w = ctx->w;
+  const int64_t Rpad = (R + 127) / 128 * 128;
+  hipStream_t st = ctx->stream;
+  int32_t n_tiles = 0;
+  rc = upload_batch_meta(ctx, offsets, n_prot, &n_tiles);
+  if (rc) return rc;
+  ctx->chunked_last = false;
   HIPCHK(hipMemsetAsync(w.node_local, 0xff, sizeof(int32_t) * Rpad, st));
   HIPCHK(hipMemsetAsync(w.node_prot, 0, sizeof(int32_t) * Rpad, st));
 
@@ -591,10 +620,10 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   // reads h3 directly
   env_threshold(ctx->down_coop, "PST_DOWN_COOP");
   const int64_t coop_max = ctx->down_coop >= 0 ? ctx->down_coop : (int64_t)(DOWN_COOP_SIMD_FRACTION * ctx->n_simds);
-  const bool down_coop = ctx->df == 1 && (int64_t)tp.size() <= coop_max;
+  const bool down_coop = ctx->df == 1 && (int64_t)n_tiles <= coop_max;
   if (!down_coop) HIPCHK(hipMemcpyAsync(w.h1, hbuf[3], sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
   pst::DownArgs d{};
-  d.n_tiles = (int32_t)tp.size();
+  d.n_tiles = n_tiles;
   d.tile_prot = w.tile_prot;
   d.tile_t0 = w.tile_t0;
   d.offsets = w.offsets;
@@ -625,9 +654,9 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     d.fsq_basis[i] = ctx->fsq_basis[i];
   }
   d.tokens_out = d_tokens;
-  d.bounded_out = w.bounded;
-  d.quant_out = w.quant;
-  d.pre_proj_out = w.pre_proj;
+  d.bounded_out = w.bounded + 8 * out_row0;
+  d.quant_out = w.quant + 8 * out_row0;
+  d.pre_proj_out = w.pre_proj + 128 * out_row0;
   if (d.n_tiles > 0) pst::launch_down(ctx->df, d, down_coop, st);
   mark(ctx, 6);
   HIPCHK(hipGetLastError());
@@ -636,7 +665,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   ctx->last_B = n_prot;
   ctx->last_tokens = d_tokens;
   ctx->last_nnodes = d_nnodes;
-  ctx->last_ntiles = (int32_t)tp.size();
+  ctx->last_ntiles = n_tiles;
   (void)d_ntok;
   return PST_OK;
 }
@@ -753,6 +782,12 @@ int pst_destroy(pst_ctx* ctx) {
   if (ctx->msg) (void)hipFree(ctx->msg);
   for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_U, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
+  if (ctx->copy_stream) {
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    (void)hipStreamDestroy(ctx->copy_stream);
+  }
+  for (hipEvent_t e : ctx->copy_ev)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return PST_OK;
@@ -785,6 +820,39 @@ int pst_tokenize_device(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flag
   return PST_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Protein-boundary chunk starts [0 = c_0 < c_1 < ... < c_n = n_prot] of a pipelined host call.
+// The first chunk is a quarter of the rest's average so that little copy time is exposed; the
+// others split the remaining residues evenly.
+std::vector<int32_t> plan_chunks(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot) {
+  const int64_t R = offsets[n_prot];
+  const int64_t tasks = (R + 31) / 32;
+  env_threshold(ctx->h2d_chunks, "PST_H2D_CHUNKS");
+  int n = ctx->h2d_chunks >= 1 ? (int)std::min<int64_t>(ctx->h2d_chunks, H2D_MAX_CHUNKS)
+                               : (int)std::min<int64_t>(H2D_MAX_CHUNKS, tasks / H2D_MIN_CHUNK_TASKS);
+  n = std::max(1, std::min(n, (int)n_prot));
+  std::vector<int32_t> cut{0};
+  if (n > 1) {
+    // weights: first chunk 1/4 of a regular chunk
+    const double unit = (double)R / (0.25 + (n - 1));
+    double target = 0.25 * unit;
+    for (int32_t b = 1; b < n_prot && (int)cut.size() < n; ++b)
+      if ((double)offsets[b] >= target) {
+        cut.push_back(b);
+        target += unit;
+      }
+  }
+  cut.push_back(n_prot);
+  return cut;
+}
+
+}  // namespace
+
+extern "C" {
+
 int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,
                  int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
   if (!ctx) return PST_E_INVALID;
@@ -797,10 +865,49 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
   rc = ensure_workspace(ctx, R, n_prot);
   if (rc) return rc;
   auto& w = ctx->w;
-  HIPCHK(hipMemcpyAsync(w.pos, atom_pos, sizeof(double) * 111 * R, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(w.flags, atom_flags, 37 * R, hipMemcpyHostToDevice, ctx->stream));
-  rc = run(ctx, w.pos, w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes);
-  if (rc) return rc;
+  const std::vector<int32_t> cut = plan_chunks(ctx, offsets, n_prot);
+  const int n_chunks = (int)cut.size() - 1;
+  if (n_chunks == 1) {
+    HIPCHK(hipMemcpyAsync(w.pos, atom_pos, sizeof(double) * 111 * R, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(w.flags, atom_flags, 37 * R, hipMemcpyHostToDevice, ctx->stream));
+    rc = run(ctx, w.pos, w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes);
+    if (rc) return rc;
+  } else {
+    // copy chunk k on copy_stream, then queue its compute behind an event; the host issues
+    // copy k+1 after compute k is queued, so even a staged (pageable) copy overlaps compute k
+    if (!ctx->copy_stream) {
+      HIPCHK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+      for (int k = 0; k < H2D_MAX_CHUNKS; ++k) HIPCHK(hipEventCreateWithFlags(&ctx->copy_ev[k], hipEventDisableTiming));
+    }
+    std::vector<int64_t> loc;
+    for (int k = 0; k < n_chunks; ++k) {
+      const int32_t b0 = cut[k], b1 = cut[k + 1];
+      const int64_t r0 = offsets[b0], r1 = offsets[b1];
+      HIPCHK(hipMemcpyAsync(w.pos + 111 * r0, atom_pos + 111 * r0, sizeof(double) * 111 * (r1 - r0),
+                            hipMemcpyHostToDevice, ctx->copy_stream));
+      HIPCHK(hipMemcpyAsync(w.flags + 37 * r0, atom_flags + 37 * r0, 37 * (r1 - r0), hipMemcpyHostToDevice,
+                            ctx->copy_stream));
+      HIPCHK(hipEventRecord(ctx->copy_ev[k], ctx->copy_stream));
+      HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->copy_ev[k], 0));
+      loc.assign(offsets + b0, offsets + b1 + 1);
+      for (auto& o : loc) o -= r0;
+      rc = run(ctx, w.pos + 111 * r0, w.flags + 37 * r0, loc.data(), b1 - b0, w.tokens + r0, w.n_tok + b0,
+               w.n_nodes + b0, false, r0);
+      if (rc) return rc;
+    }
+    // the batch as a whole for pst_aux / pst_codebook_aux: offsets, token tiles and last_* of all
+    // chunks (the chunks' own metadata uploads were stream-ordered before this one)
+    int32_t n_tiles = 0;
+    rc = upload_batch_meta(ctx, offsets, n_prot, &n_tiles);
+    if (rc) return rc;
+    ctx->last_R = R;
+    ctx->last_Rpad = (R + 127) / 128 * 128;
+    ctx->last_B = n_prot;
+    ctx->last_tokens = w.tokens;
+    ctx->last_nnodes = w.n_nodes;
+    ctx->last_ntiles = n_tiles;
+    ctx->chunked_last = true;
+  }
   hipLaunchKernelGGL(k_ntok, dim3((n_prot + 255) / 256), dim3(256), 0, ctx->stream, w.n_nodes, w.n_tok, n_prot, ctx->df);
   HIPCHK(hipMemcpyAsync(tokens_out, w.tokens, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, ctx->stream));
   if (n_tokens_out)
@@ -991,6 +1098,8 @@ int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t
 
 int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes) {
   if (!ctx || ctx->last_R == 0) return PST_E_INVALID;
+  if (ctx->chunked_last)
+    return fail(ctx, PST_E_INVALID, "the last call was pipelined in chunks (PST_H2D_CHUNKS=1 keeps intermediates)");
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   const int64_t Rp = ctx->last_Rpad;

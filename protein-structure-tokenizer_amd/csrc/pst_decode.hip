@@ -1343,10 +1343,10 @@ int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* 
   dec->desc = *desc;
   dec->D = D;
   dec->df = df;
-  auto bad = [&](const char* what) {
+  auto bad = [&](const char* what, int code = PST_E_HIP) {
     g_dec_create_error = what;
     pst_decoder_destroy(dec);
-    return PST_E_HIP;
+    return code;
   };
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&dec->stream, hipStreamNonBlocking) != hipSuccess)
     return bad("hip stream creation failed");
@@ -1371,15 +1371,15 @@ int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* 
       return bad("IPA projection buffer allocation failed");
     int col = 0;
     for (const Lin* L : {&dec->W.q_scalar, &dec->W.kv_scalar, &dec->W.q_point, &dec->W.kv_point}) {
-      if (L->in != 384 ||
-          hipMemcpy2D(dec->d_ipa_w + col, 1152 * sizeof(float), L->w, L->out * sizeof(float), L->out * sizeof(float),
+      if (L->in != 384) return bad("IPA projection input width is not 384", PST_E_INVALID);
+      if (hipMemcpy2D(dec->d_ipa_w + col, 1152 * sizeof(float), L->w, L->out * sizeof(float), L->out * sizeof(float),
                       384, hipMemcpyDeviceToDevice) != hipSuccess ||
           (L->b ? hipMemcpy(dec->d_ipa_b + col, L->b, L->out * sizeof(float), hipMemcpyDeviceToDevice)
                 : hipMemset(dec->d_ipa_b + col, 0, L->out * sizeof(float))) != hipSuccess)
         return bad("IPA projection weight packing failed");
       col += L->out;
     }
-    if (col != 1152) return bad("IPA projection widths do not add up to 1152");
+    if (col != 1152) return bad("IPA projection widths do not add up to 1152", PST_E_INVALID);
   }
   // host-side constants: PE tables, levels, IPA point weights
   auto up = [&](float** d, const std::vector<float>& h) {
@@ -1447,8 +1447,6 @@ int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* 
     if (T < 0 || T > max_tok)
       return dfail(dec, PST_E_INVALID, "protein " + std::to_string(b) + ": token count outside [0, " +
                                            std::to_string(max_tok) + "]");
-    for (int64_t t = token_offsets[b]; t < token_offsets[b + 1]; ++t)
-      if ((int64_t)tokens[t] >= K) return dfail(dec, PST_E_INVALID, "token id out of range for the codebook");
   }
   DCHK(hipSetDevice(dec->device));
   Scratch S;
@@ -1473,7 +1471,10 @@ int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* 
       if (G.B > 0 && (G.N + N > kNodeCap || G.NP + N * N > kPairCap)) break;
       if (n_nodes_out) n_nodes_out[b] = (int32_t)N;
       if (T > 0) {  // empty proteins take no rows
-        G.tokens.insert(G.tokens.end(), tokens + token_offsets[b], tokens + token_offsets[b + 1]);
+        // indexes_to_codes extracts digits as (id // basis_d) mod L_d (quantize.py:70-79), which
+        // decodes any uint32 id as id mod K: ids >= K are accepted, not rejected
+        for (int64_t t = token_offsets[b]; t < token_offsets[b + 1]; ++t)
+          G.tokens.push_back((uint32_t)((uint64_t)tokens[t] % (uint64_t)K));
         G.tok_prot.insert(G.tok_prot.end(), (size_t)T, G.B);
         G.node_prot.insert(G.node_prot.end(), (size_t)N, G.B);
         G.T += T;

@@ -4,7 +4,7 @@
 //   k_prep       block/protein: backbone filter + compaction, frames, centroids, CA
 //                (preprocessing.py:69-149, quat_affine.py:406-522)
 //   k_knn        wave/receiver: float64 cdist row, ordered k-NN selection, 27 edge features
-//                (protein_utils.py:636-749; padding semantics preprocessing.py:191-271)
+//                (protein_utils.py:325-438; padding semantics preprocessing.py:191-271)
 //   k_mpnn<0..2> wave/32 receivers (1600 edge slots = 50 MFMA blocks of 32 edges): fused
 //                edge update of layer l-1 + message MLP of layer l + ordered segment sum +
 //                node update (masked LN, 128->512->128 FFN, masked LN) + the next layer's node
@@ -57,7 +57,7 @@ __device__ __forceinline__ void make_frame(const double* N, const double* CA, co
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) M[i][j] = nr[i][0] * cr[0][j] + nr[i][1] * cr[1][j] + nr[i][2] * cr[2][j];
-  // stored rows: [n | u | v] = [M2 | M0 | M1]  (basis_matrices order, protein_utils.py:717)
+  // stored rows: [n | u | v] = [M2 | M0 | M1]  (basis_matrices order, protein_utils.py:406-408)
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     out[k] = M[2][k];
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(512) void k_prep(PrepArgs a) {
 
 // ---------------------------------------------------------------------------- k_knn
 __device__ __forceinline__ double dot3(const double* b, const double* x) {
-  // numpy einsum's evaluation order for the 3-term contraction (protein_utils.py:722-733)
+  // numpy einsum's evaluation order for the 3-term contraction (protein_utils.py:411-423)
   return ((0.0 + b[0] * x[0]) + b[2] * x[2]) + b[1] * x[1];
 }
 
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
     d[i] = s < n ? cen_dist(a.cen, g, base + s) : __builtin_inf();
   }
   const int keep = n <= KNN ? n : KNN + 1;
-  const int drop = n <= KNN ? 0 : 1;  // column 0 (self) dropped when n > k (protein_utils.py:700)
+  const int drop = n <= KNN ? 0 : 1;  // column 0 (self) dropped when n > k (protein_utils.py:385-389)
   int my_s = -1;
   double my_d = 0.0;
 #ifndef PST_KNN_ROUNDS

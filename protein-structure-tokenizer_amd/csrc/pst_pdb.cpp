@@ -165,7 +165,7 @@ int atom_index(const char* name) {
 
 void parse_one(const char* text, size_t len, char chain_filter, Parsed* out) {
   int models = 0;
-  bool seen_atom_before_model = false, in_first = true;
+  bool seen_atom_before_model = false, in_first = true, started = false;
   std::vector<Chain> chains;
   size_t p = 0;
   while (p < len) {
@@ -174,20 +174,24 @@ void parse_one(const char* text, size_t len, char chain_filter, Parsed* out) {
     const char* line = text + p;
     const int ll = (int)(q - p);
     p = (q + 1 < len && text[q] == '\r' && text[q + 1] == '\n') ? q + 2 : q + 1;  // \n, \r\n or \r
-    auto starts = [&](const char* pre) {
-      size_t n = strlen(pre);
-      return (size_t)ll >= n && !memcmp(line, pre, n);
-    };
-    if (starts("MODEL")) {
+    // Bio names a record by its exact first 6 columns; its header ends at the first ATOM/HETATM/
+    // MODEL record and the atomic data at the first CONECT or "END   " record
+    auto rec = [&](const char* name6) { return ll >= 6 && !memcmp(line, name6, 6); };
+    const bool is_atom = rec("ATOM  "), is_het = rec("HETATM"), is_model = rec("MODEL ");
+    if (!started) {
+      if (!is_atom && !is_het && !is_model) continue;
+      started = true;
+    }
+    if (rec("CONECT") || rec("END   ")) break;
+    if (is_model) {
       ++models;
       in_first = models == 1;
       continue;
     }
-    if (starts("ENDMDL")) {
+    if (rec("ENDMDL")) {
       in_first = false;
       continue;
     }
-    const bool is_atom = starts("ATOM"), is_het = starts("HETATM");
     if (!is_atom && !is_het) continue;
     if (models == 0) seen_atom_before_model = true;
     if (!in_first && models > 0) continue;

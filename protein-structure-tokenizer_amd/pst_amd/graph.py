@@ -16,7 +16,7 @@ C-alpha coordinates. `pad_protein_graph` applies the padding of
   tokens_mask [512 / df, 1]               bool
   senders, receivers [25600]              int64, padded as the reference pads them
 """
-from typing import List, NamedTuple, Sequence
+from typing import List, NamedTuple, Optional, Sequence
 
 import numpy as np
 
@@ -96,11 +96,32 @@ def build_protein_graphs(tokenizer, samples: Sequence[ProteinStructureSample],
 
 
 _GRAPH_CTX = {}
+_GRAPH_DEVICE = [None]
 
 
-def _graph_context(device: int = 0):
+def set_graph_device(device: Optional[int]) -> None:
+    """The GPU that builds `ProteinGraph`s on demand (`ProteinGraphView.graph`,
+    `preprocess_sample`). `InferenceRunner.prepare_tokenize_fn` sets it to the runner's first
+    device; None restores the default (LOCAL_RANK modulo the visible devices, else 0)."""
+    _GRAPH_DEVICE[0] = device
+
+
+def graph_device() -> int:
+    if _GRAPH_DEVICE[0] is not None:
+        return _GRAPH_DEVICE[0]
+    import os
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if local == 0:
+        return 0
+    from . import _native
+    return local % max(1, _native.device_count())
+
+
+def _graph_context(device: Optional[int] = None):
     """A libpst context used only for graph builds (the encoder weights do not enter the graph,
-    so they are zeros)."""
+    so they are zeros), on `device` or the caller's graph device (`graph_device()`)."""
+    if device is None:
+        device = graph_device()
     if device not in _GRAPH_CTX:
         from . import _native, params
         blob = np.zeros(params.param_count(6), np.float32)
@@ -111,7 +132,8 @@ def _graph_context(device: int = 0):
 class ProteinGraphView:
     """What `runner.make_graph_from_pdb` returns: the parsed structure, which the tokenize path
     hands to the GPU as is, that also reads as the reference's padded `ProteinGraph` — the
-    `ProteinGraph` fields are built on first access (pst_build_graph on GPU 0) and cached.
+    `ProteinGraph` fields are built on first access (pst_build_graph on `graph_device()`, the
+    runner's device) and cached.
     Other attributes (`nb_residues`, `atom37_positions`, ...) are the structure's."""
 
     __slots__ = ("sample", "downsampling_ratio", "_graph")

@@ -3,6 +3,9 @@
 
 Biopython is not part of this build, so the PDB fixed-column format is read directly with the
 semantics `Bio.PDB.PDBParser(QUIET=True)` gives the reference:
+  * records are named by their exact first 6 columns ("ATOM  ", "HETATM", "MODEL ", "ENDMDL");
+    the header ends at the first ATOM/HETATM/MODEL record and coordinates end at the first
+    "CONECT" or "END   " record (Bio's `_get_header` / `_parse_coordinates`);
   * only the first MODEL exists, or ValueError("Only single model PDBs ...") for >1 model;
   * ATOM and HETATM records both create residues (waters included), grouped per chain in order
     of first appearance, residues in file order, keyed by (het-flag, resseq, icode);
@@ -27,16 +30,23 @@ def _parse_records(pdb_str: str):
     seen_atom_before_model = False
     chains: "OrderedDict[str, OrderedDict]" = OrderedDict()
     in_first = True
+    started = False  # Bio's header ends at the first "ATOM  " / "HETATM" / "MODEL " record
     for line in pdb_str.splitlines():
-        rec = line[:6]
-        if rec.startswith("MODEL"):
+        rec = line[:6]  # Bio compares the 6-column record name exactly
+        if not started:
+            if rec not in ("ATOM  ", "HETATM", "MODEL "):
+                continue
+            started = True
+        if rec in ("END   ", "CONECT"):
+            break  # end of atomic data: Bio stops reading coordinates here
+        if rec == "MODEL ":
             models += 1
             in_first = models == 1
             continue
-        if rec.startswith("ENDMDL"):
+        if rec == "ENDMDL":
             in_first = False
             continue
-        if not (rec.startswith("ATOM") or rec.startswith("HETATM")):
+        if rec not in ("ATOM  ", "HETATM"):
             continue
         if models == 0:
             seen_atom_before_model = True

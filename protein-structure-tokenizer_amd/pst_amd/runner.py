@@ -156,16 +156,19 @@ class TokenizeFn:
         self._pool = _cf.ThreadPoolExecutor(max_workers=max(1, len(self.devices)))
 
     def _context(self, model_params: ReplicatedParams, dev: int) -> _native.Tokenizer:
+        # the entry keeps the params object alive, so its id cannot be reused by other weights
+        # while the context built from it is cached
         key = (id(model_params), dev)
-        t = self._ctx.get(key)
-        if t is None:
+        ent = self._ctx.get(key)
+        if ent is None or ent[0] is not model_params:
             levels = self.cfg.levels
             if len(levels) != model_params.codes_dim:
                 raise ValueError(f"params have codes_dimension {model_params.codes_dim}, config levels {levels}")
             t = _native.Tokenizer(dev, self.cfg.codebook_size, self.cfg.downsampling_ratio,
                                   model_params.blob, levels)
-            self._ctx[key] = t
-        return t
+            ent = (model_params, t)
+            self._ctx[key] = ent
+        return ent[1]
 
     def __call__(self, model_params: ReplicatedParams, random_key: Any, batched_graph: ProteinBatch) -> Dict[str, np.ndarray]:
         n_dev = batched_graph.batch_dims[0]
@@ -234,7 +237,7 @@ class TokenizeFn:
         return o
 
     def close(self):
-        for t in self._ctx.values():
+        for _, t in self._ctx.values():
             t.close()
         self._ctx.clear()
         self._pool.shutdown(wait=True)
@@ -276,6 +279,8 @@ class InferenceRunner:
         """`emit_aux=True` also returns the other QuantizerOutput fields (quantize,
         straight_through_quantized, continuous_embedding, continuous_embedding_pre_proj,
         distances, soft_proba, perplexity) shaped [n_dev, bpd, seq_max/df, ...] as the reference."""
+        from .graph import set_graph_device
+        set_graph_device(list(devices)[0])  # on-demand ProteinGraph builds run on this runner's GPU
         return TokenizeFn(cfg, devices, emit_aux)
 
     @staticmethod
@@ -427,13 +432,14 @@ class DecodeFn:
         self._pool = _cf.ThreadPoolExecutor(max_workers=max(1, len(self.devices)))
 
     def _context(self, model_params: ReplicatedParams, dev: int):
-        key = (id(model_params), dev)
-        d = self._ctx.get(key)
-        if d is None:
+        key = (id(model_params), dev)  # strong ref in the entry: see TokenizeFn._context
+        ent = self._ctx.get(key)
+        if ent is None or ent[0] is not model_params:
             blob = _params.pack_decoder(model_params.params, model_params.codes_dim)
-            d = _native.Decoder(dev, self.cfg.codebook_size, self.cfg.downsampling_ratio, blob, self.cfg.levels)
-            self._ctx[key] = d
-        return d
+            ent = (model_params, _native.Decoder(dev, self.cfg.codebook_size, self.cfg.downsampling_ratio,
+                                                 blob, self.cfg.levels))
+            self._ctx[key] = ent
+        return ent[1]
 
     def __call__(self, model_params: ReplicatedParams, random_key: Any, tokens: np.ndarray,
                  tokens_mask: np.ndarray) -> Dict[str, np.ndarray]:
@@ -457,7 +463,7 @@ class DecodeFn:
         return {"final_atom_positions": pos, "final_atom_mask": mask, "n_nodes": df * n_tok}
 
     def close(self):
-        for d in self._ctx.values():
+        for _, d in self._ctx.values():
             d.close()
         self._ctx.clear()
         self._pool.shutdown(wait=True)

@@ -26,3 +26,14 @@ class ProteinStructureSample(NamedTuple):
         """Packed per-atom flags handed to the device: bit0 = gt_exists, bit1 = atom_exists."""
         return (self.atom37_gt_exists.astype(np.uint8)
                 | (self.atom37_atom_exists.astype(np.uint8) << 1))
+
+
+def sample_from_arrays(positions: np.ndarray, flags: np.ndarray, aatype_idx=None) -> ProteinStructureSample:
+    """Inverse of `atom_flags`: a sample from atom37 positions + packed flags (aatype ALA unless
+    given as residue indices; the tokenize path never reads it)."""
+    n = positions.shape[0]
+    aa = np.zeros((n, rc.restype_num + 1))
+    idx = np.full(n, rc.restype_order["A"]) if aatype_idx is None else np.asarray(aatype_idx)
+    aa[np.arange(n), idx] = 1.0
+    return ProteinStructureSample(None, n, aa, np.asarray(positions, dtype=np.float64),
+                                  (flags & 1).astype(bool), (flags & 2).astype(bool), 0.0, 1)

@@ -12,8 +12,11 @@ used directly (`pst_amd.config.tokenizer_config`); with it, the reference's YAML
 composed the same way the reference does (`config_overrides` from the two flags).
 
 One process drives every local GPU (a host thread per GPU, like the reference's pmap). Under
-`torchrun` (WORLD_SIZE > 1) each rank instead takes GPU LOCAL_RANK and a round-robin shard of
-the PDB list; there is no collective on the data path.
+`torchrun` (WORLD_SIZE > 1) each rank instead takes GPU LOCAL_RANK (modulo the visible devices)
+and an LPT shard of the PDB list balanced on file size (`runner.shard_for_rank`); there is no
+collective on the data path. Rank 0 creates `--token_save_path` exactly as the reference does
+(`inference_runner.py:265`, FileExistsError if it exists) and broadcasts the outcome over a gloo
+group before any rank starts; each rank writes through a private `.rank<N>` directory inside it.
 """
 import argparse
 import os
@@ -41,7 +44,8 @@ def main(pdbs: List[str], token_save_path: str, backend: str, batch_size_per_dev
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         rank = int(os.environ.get("RANK", "0"))
-        local_devices = [int(os.environ.get("LOCAL_RANK", "0"))]
+        _create_output_on_rank0(token_save_path, rank)
+        local_devices = [int(os.environ.get("LOCAL_RANK", "0")) % n_local_device]
         # LPT on PDB text size (∝ atoms ∝ residues) balances residues per GPU
         pdbs = sorted(pdbs)
         pdbs = shard_for_rank(pdbs, rank, world, weights=[os.path.getsize(p) for p in pdbs])
@@ -60,9 +64,30 @@ def main(pdbs: List[str], token_save_path: str, backend: str, batch_size_per_dev
         tokenize.close()
 
 
+def _create_output_on_rank0(token_save_path: str, rank: int) -> None:
+    """`os.makedirs(token_save_path, exist_ok=False)` once for the job (inference_runner.py:265):
+    rank 0 creates it, every rank raises the same FileExistsError if it already existed."""
+    import torch.distributed as dist
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo")  # env:// from torchrun; control only, no data
+    try:
+        msg = [None]
+        if rank == 0:
+            try:
+                os.makedirs(token_save_path, exist_ok=False)
+            except FileExistsError as e:
+                msg = [str(e)]
+        dist.broadcast_object_list(msg, src=0)
+        if msg[0] is not None:
+            raise FileExistsError(msg[0])
+    finally:
+        if own:
+            dist.destroy_process_group()
+
+
 def _tokenize_rank(runner, tokenize, model_params, pdbs, token_save_path, cfg, bs):
-    # every rank writes into the same directory; rank files are disjoint by construction
-    os.makedirs(token_save_path, exist_ok=True)
+    # every rank writes into the directory rank 0 created; rank files are disjoint by construction
     tmp = os.path.join(token_save_path, f".rank{os.environ.get('RANK', '0')}")
     runner.tokenize(random_key=None, quantize=tokenize, model_params=model_params, pdbs=pdbs,
                     token_save_path=tmp, num_device=1, data_config=cfg, batch_size_per_device=bs)

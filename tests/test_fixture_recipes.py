@@ -1,0 +1,40 @@
+"""Fixture recipes cannot drift from the committed data: the synthetic inputs of
+`forward_ref_wide.npz` are regenerated with today's `pst_amd.synthetic` and must hash to the
+SHA-256 stored beside them; the other fixtures' generators read their stored inputs back
+(`make_golden.py forward` reuses `forward_golden_f64.npz`'s inputs when the file exists)."""
+import numpy as np
+
+import make_forward_wide as M
+import refwide
+from pst_amd import synthetic
+
+F = refwide.load()
+
+
+def test_wide_synthetic_inputs_reproduce():
+    checked = 0
+    for c in refwide.cases(F):
+        if c + "/input_sha256" not in F.files:
+            continue
+        n_res, seed = (int(v) for v in F[c + "/synthetic_args"])
+        s = synthetic.synthetic_protein(n_res, seed)
+        pos, fl = s.atom37_positions.astype(np.float32), s.atom_flags()
+        assert M.input_sha(pos, fl) == str(F[c + "/input_sha256"]), c
+        assert np.array_equal(pos, F[c + "/in_positions"]) and np.array_equal(fl, F[c + "/in_flags"])
+        checked += 1
+    assert checked == 10
+
+
+def test_bench_workload_is_the_fixture_workload():
+    """bench.py's proteins 0..7 (seed 1000 + p, 256 residues) are the fixture's bench256 cases."""
+    b = synthetic.synthetic_batch(2, 256, seed=1000)
+    for p, s in enumerate(b):
+        assert np.array_equal(s.atom37_positions.astype(np.float32), F[f"bench256_p{p}_k4096_df1/in_positions"])
+
+
+def test_casp14_inputs_match_atom37_fixture():
+    C = np.load(M.os.path.join(M.HERE, "casp14_atom37.npz"))
+    for i, nm in enumerate(C["names"]):
+        a, b = int(C["offsets"][i]), int(C["offsets"][i + 1])
+        for cb in (4096, 64000):
+            assert np.array_equal(F[f"casp_{nm}_k{cb}_df1/in_positions"], C["positions"][a:b])

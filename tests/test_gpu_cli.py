@@ -85,9 +85,11 @@ def test_tokenize_fn_emit_aux_matches_reference_golden():
     np.testing.assert_allclose(out["soft_proba"][0, 0, T:].sum(-1), 1.0, rtol=1e-5)
 
 
-@pytest.mark.parametrize("subset", ["T1024", "all"])
-def test_cli_casp14(tmp_path, casp14_dir, subset):
-    """SURVEY configs 1 (T1024, 391 tokens) and 2 (all 31 structures) through the drop-in CLI."""
+@pytest.mark.parametrize("subset,cb", [("T1024", 4096), ("all", 4096), ("all", 64000)])
+def test_cli_casp14(tmp_path, casp14_dir, subset, cb):
+    """SURVEY configs 1 (T1024, 391 tokens), 2 (all 31 structures) and 4 (all 31 at codebook
+    64 000, df 1) through the drop-in CLI: token files equal to the oracle's and to the
+    reference's own float64 forward on the same weights (`forward_ref_wide.npz`)."""
     import shutil
     sys.path.insert(0, SCRIPTS)
     import tokenize_pdb
@@ -98,19 +100,22 @@ def test_cli_casp14(tmp_path, casp14_dir, subset):
         shutil.copy(os.path.join(casp14_dir, nm + ".pdb"), pdb_dir / (nm + ".pdb"))
     mdir = tmp_path / "model"
     mdir.mkdir()
-    full = P.random_full_params(6, seed=8)
+    full = P.random_full_params(6, seed=1234)  # encoder half = the reference fixture's weights
     P.save_params_npz(str(mdir / "params.npz"), full)
     out = tmp_path / "tokens"
     tokenize_pdb.cli(["--pdb_dir", str(pdb_dir), "--token_save_path", str(out), "--batch_size_per_device", "8",
-                      "--weights_dir", str(mdir)])
+                      "--weights_dir", str(mdir), "--codebook_size", str(cb)])
     blob = P.pack(full, 6)
+    import refwide
+    R = refwide.load()
     F = np.load(os.path.join(os.path.dirname(__file__), "golden", "casp14_atom37.npz"))
     idx = {str(n): i for i, n in enumerate(F["names"])}
     for nm in names:
         i = idx[nm]
         a, b = int(F["offsets"][i]), int(F["offsets"][i + 1])
-        want = O.tokenize(blob, C.LEVELS[4096], 1, F["positions"][a:b].astype(np.float64), F["flags"][a:b])["tokens"]
+        want = O.tokenize(blob, C.LEVELS[cb], 1, F["positions"][a:b].astype(np.float64), F["flags"][a:b])["tokens"]
         t = np.load(out / f"{nm}_tokens.npy")
         assert np.array_equal(t[0], want), nm
+        assert np.array_equal(t[0], R[f"casp_{nm}_k{cb}_df1/tokens"]), nm
     if subset == "T1024":
         assert np.load(out / "T1024_tokens.npy").shape == (1, 391)

@@ -109,6 +109,19 @@ def test_grouped_decode_matches_single():
     dec.close()
 
 
+def test_token_ids_beyond_codebook_wrap_like_reference():
+    """indexes_to_codes (quantize.py:70-79) extracts digits as (id // basis) mod L, so an id >= K
+    decodes as id mod K; the decoder accepts such ids instead of rejecting them."""
+    from pst_amd._native import Decoder
+    rng = np.random.default_rng(3)
+    ids = rng.integers(0, 4096, 40).astype(np.uint32)
+    dec = Decoder(0, 4096, 1, P.pack_decoder(P.random_full_params(6, 4), 6))
+    a = dec.decode([ids])[0]
+    b = dec.decode([ids + np.uint32(4096 * 3)])[0]
+    dec.close()
+    assert np.array_equal(a, b)
+
+
 def test_fused_pair_kernel_matches_library_path(monkeypatch):
     """k_pair_fused (one kernel over 32-pair tiles) against the library-GEMM pair path
     (PST_DECODE_UNFUSED=1) on the same tokens: pair representation and atoms agree to float32

@@ -1,0 +1,49 @@
+"""pst_tokenize's H2D pipeline (protein chunks copied on a second stream while the previous
+chunk computes) gives the same bits as the one-shot call: token ids, n_tokens / n_nodes, the
+aux outputs and the codebook aux (distances, argmin, histogram) over the whole batch."""
+import os
+
+import numpy as np
+import pytest
+
+from pst_amd import params as P
+from pst_amd import synthetic
+from pst_amd._native import pack_samples
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(chunks, cb=4096, df=1):
+    from pst_amd._native import Tokenizer
+    os.environ["PST_H2D_CHUNKS"] = str(chunks)  # read at the context's first call
+    t = Tokenizer(0, cb, df, P.random_blob(6, 1234))
+    return t
+
+
+@pytest.mark.parametrize("cb,df", [(4096, 1), (64000, 4)])
+def test_chunked_h2d_is_bitwise_identical(cb, df):
+    rng = np.random.default_rng(7)
+    lens = [int(x) for x in rng.integers(50, 513, 40)]
+    samples = [synthetic.synthetic_protein(n, 900 + i) for i, n in enumerate(lens)]
+    pos, flags, off = pack_samples(samples)
+    R = int(off[-1])
+    outs = []
+    for chunks in (1, 3, 8):
+        t = _ctx(chunks, cb, df)
+        tok, nt, nn = t.tokenize_packed(pos, flags, off)
+        tok2, _, _ = t.tokenize_packed(pos, flags, off)  # a second call on the same context
+        aux = t.aux(R)
+        T = int(nt.sum())
+        ca = t.codebook_aux(T, distances=True, soft_proba=False)
+        outs.append((tok, nt, nn, aux, ca))
+        assert np.array_equal(tok, tok2)
+        t.close()
+    os.environ.pop("PST_H2D_CHUNKS")
+    base = outs[0]
+    for o in outs[1:]:
+        assert np.array_equal(o[0], base[0]) and np.array_equal(o[1], base[1]) and np.array_equal(o[2], base[2])
+        for k in ("bounded", "quantize", "pre_proj"):
+            assert np.array_equal(o[3][k].view(np.uint32), base[3][k].view(np.uint32)), k
+        assert np.array_equal(o[4]["argmin"], base[4]["argmin"])
+        assert np.array_equal(o[4]["histogram"], base[4]["histogram"])
+        assert np.array_equal(o[4]["distances"].view(np.uint32), base[4]["distances"].view(np.uint32))

@@ -1,0 +1,60 @@
+"""GPU token ids vs the REFERENCE's own forward on the benchmarked configs (`forward_ref_wide.npz`:
+reference `Vq3D.encode_and_quantize`, model.py:453-479, in float64 under the shim) — all 31
+CASP14 proteins at codebook 4096 and 64 000 (BASELINE configs 2 and 4), the first 8 proteins of
+the bench workload (config 3), 2 × 512 residues at 64 000 / df 4 (config 5) and the < 50-residue
+branch. Through the C ABI (pst_tokenize + pst_aux).
+
+Bar: token ids identical; a mismatch is tolerated only where the reference's latent sits closer
+to a rounding boundary than our float32 deviation from it at that dim (then it is rounding noise
+of float32 vs float64, `refwide.report`), and none has occurred (13 606 of 13 606 equal on the
+oracle, which the GPU matches bit for bit).
+"""
+import numpy as np
+import pytest
+
+import refwide
+from pst_amd import params as P
+
+pytestmark = pytest.mark.gpu
+F = refwide.load()
+# vs the JAX-float32-PE rendering (see test_oracle_wide.py), measured on the oracle = GPU bits:
+# pre-projection ≤ 3.0e-7, bounded ≤ 1.04e-5; vs the all-float64 rendering ≤ 6.1e-6 / 1.5e-4
+TOL = {"_pe32": (1e-6, 3e-5), "": (1.5e-5, 4e-4)}
+
+
+def _make(cb, df, D, seed):
+    from pst_amd._native import Tokenizer
+    return Tokenizer(0, cb, df, P.random_blob(D, seed))
+
+
+@pytest.fixture(scope="module")
+def gpu_out():
+    return refwide.device_outputs(F, _make)
+
+
+@pytest.mark.parametrize("var", ["_pe32", ""])
+@pytest.mark.parametrize("prefix", ["casp_T", "bench256_", "bench512_", "short_"])
+def test_gpu_tokens_equal_reference(gpu_out, prefix, var):
+    reps = []
+    tol_pre, tol_b = TOL[var]
+    for c in refwide.cases(F, prefix):
+        tok, b, pp = gpu_out[c]
+        assert np.abs(b - F[c + "/bounded" + var]).max() < tol_b, c
+        if c + "/pre_proj" + var in F.files:
+            assert np.abs(pp - F[c + "/pre_proj" + var]).max() < tol_pre, c
+        r = refwide.report(F[c + "/bounded" + var], F[c + "/tokens" + var], b, tok)
+        assert r["mismatches_explained_by_rounding"], (c, r)
+        reps.append(r)
+    r = refwide.merge(reps)
+    print(prefix, var, {k: r[k] for k in ("tokens", "identical", "min_margin", "max_deviation",
+                                          "max_deviation_over_margin")})
+    assert r["identical"] == r["tokens"], r
+
+
+def test_gpu_config4_casp14_k64000():
+    """Config 4 on its own: the 31 CASP14 proteins in ONE batch at codebook 64 000, df 1."""
+    out = refwide.device_outputs(F, _make, prefix="casp_")
+    names = [c for c in refwide.cases(F, "casp_") if "_k64000_" in c]
+    assert len(names) == 31
+    for c in names:
+        assert np.array_equal(out[c][0], F[c + "/tokens"]), c

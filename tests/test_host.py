@@ -266,7 +266,19 @@ def _edge_texts():
         "crlf": "\r\n".join(_res("A", 1) + _res("A", 2, base=3.0)),
         "empty": "HEADER    nothing\nEND\n",
         "same_key_het_vs_atom": "\n".join(_res("A", 5) + _res("A", 5, "GLY", base=2.0, rec="HETATM")),
+        # Bio stops reading coordinates at the first CONECT / "END   " record after the header
+        "after_conect": "\n".join(_res("A", 1) + ["CONECT    1    2"] + _res("A", 2, base=3.0, rec="HETATM")),
+        "after_padded_end": "\n".join(_res("A", 1) + ["END   "] + _res("A", 2, base=3.0)),
+        "after_bare_end": "\n".join(_res("A", 1) + ["END"] + _res("A", 2, base=3.0)),
+        "conect_in_header": "\n".join(["CONECT    1    2", "END   "] + _res("A", 1) + _res("A", 2, base=3.0)),
+        "record_prefix_only": "\n".join(_res("A", 1) + [l.replace("ATOM  ", "ATOMS ") for l in _res("A", 2, base=3.0)]),
     }
+
+
+@pytest.mark.parametrize("case,n", [("after_conect", 1), ("after_padded_end", 1), ("after_bare_end", 2),
+                                    ("conect_in_header", 2), ("record_prefix_only", 1)])
+def test_parser_record_names_and_end_of_coordinates(case, n):
+    assert _both(_edge_texts()[case]).nb_residues == n
 
 
 @pytest.mark.parametrize("case", sorted(_edge_texts()))

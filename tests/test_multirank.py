@@ -54,6 +54,31 @@ def test_two_rank_cli_sharding(tmp_path):
         assert np.array_equal(t[0], want)
 
 
+def test_two_rank_cli_existing_output_dir(tmp_path):
+    """Rank 0 creates --token_save_path with exist_ok=False; if it exists, every rank raises."""
+    import _mr_worker
+    pdb_dir = tmp_path / "pdbs"
+    pdb_dir.mkdir()
+    (pdb_dir / "p0.pdb").write_text(pdb.to_pdb_string(synthetic.synthetic_protein(55, 3)))
+    mdir = tmp_path / "model"
+    mdir.mkdir()
+    P.save_params_npz(str(mdir / "params.npz"), P.random_full_params(6, seed=21))
+    out = tmp_path / "tok"
+    out.mkdir()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mr_worker.run_existing_dir, args=(r, 2, port, str(pdb_dir), str(mdir), str(out), q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert got == [(0, "FileExistsError"), (1, "FileExistsError")]
+    assert os.listdir(out) == []
+
+
 def test_global_perplexity_two_ranks():
     """The cross-rank perplexity (one all-reduce) equals the single-process pmean formula."""
     import _mr_worker

@@ -1,0 +1,81 @@
+"""The CPU oracle against the reference's own forward on the benchmarked configs.
+
+`forward_ref_wide.npz` (`golden/make_forward_wide.py`): the reference `Vq3D.encode_and_quantize`
+(model.py:453-479) in float64 under the shim on all 31 CASP14 proteins at codebook 4096 and
+64 000 (df 1; BASELINE configs 2 and 4), the first 8 proteins of the bench workload (256
+residues, config 3), 2 × 512 residues at 64 000 / df 4 (config 5) and the < 50-residue branch —
+13 606 tokens. The oracle executes the canonical float32 sequence the GPU executes bit for bit
+(DESIGN.md §4), so this pins the GPU's arithmetic to the reference; the GPU side is
+`test_gpu_reference_wide.py`.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import refwide
+from oracle import oracle as O
+from pst_amd import params as P
+from pst_amd.config import LEVELS
+
+F = refwide.load()
+# Two float64 renderings of the reference (make_forward_wide.py): "pe32" evaluates the sinusoidal
+# PE argument in float32 as JAX does with x64 off (the real reference's value), the other in
+# float64. Measured over all 75 cases (oracle = GPU bits):
+#   vs pe32: pre-projection (unit norm, 128-d) ≤ 3.0e-7, bounded latents (|b| < 3.5) ≤ 1.04e-5
+#   vs f64:  ≤ 6.1e-6 and ≤ 1.5e-4 — the PE argument's own float32 rounding, not our arithmetic
+TOL = {"_pe32": (1e-6, 3e-5), "": (1.5e-5, 4e-4)}
+
+
+def _run(c):
+    n, T, cb, df, D, seed = (int(v) for v in F[c + "/meta"])
+    out = O.tokenize(P.random_blob(D, seed), LEVELS[cb], df, F[c + "/in_positions"].astype(np.float64),
+                     F[c + "/in_flags"])
+    return c, out
+
+
+@pytest.fixture(scope="module")
+def oracle_outputs():
+    with ThreadPoolExecutor(8) as ex:  # the C oracle releases the GIL
+        return dict(ex.map(_run, refwide.cases(F)))
+
+
+@pytest.mark.parametrize("var", ["_pe32", ""])
+@pytest.mark.parametrize("prefix", ["casp_", "bench256_", "bench512_", "short_"])
+def test_oracle_tokens_equal_reference_wide(oracle_outputs, prefix, var):
+    reps = []
+    tol_pre, tol_b = TOL[var]
+    for c in refwide.cases(F, prefix):
+        n, T, cb, df, D, seed = (int(v) for v in F[c + "/meta"])
+        out = oracle_outputs[c]
+        assert out["graph"]["n"] == n and len(out["tokens"]) == T
+        assert np.abs(out["b"] - F[c + "/bounded" + var]).max() < tol_b, c
+        if c + "/pre_proj" + var in F.files:
+            assert np.abs(out["pre_proj"] - F[c + "/pre_proj" + var]).max() < tol_pre, c
+        reps.append(refwide.report(F[c + "/bounded" + var], F[c + "/tokens" + var], out["b"], out["tokens"]))
+    r = refwide.merge(reps)
+    assert r["mismatches_explained_by_rounding"], r
+    assert r["identical"] == r["tokens"], r
+
+
+def test_fixture_margin_fields():
+    for c in refwide.cases(F):
+        for var in ("", "_pe32"):
+            m = refwide.dim_margins(F[c + "/bounded" + var]).min(-1)
+            assert np.array_equal(m, F[c + "/margin" + var])
+        # the two renderings agree on every token id of the fixture
+        assert np.array_equal(F[c + "/tokens"], F[c + "/tokens_pe32"])
+
+
+def test_reference_as_computed_torch_matches_fixture():
+    """oracle/reference_as_computed.py (the reference's padded, dense computation in plain
+    PyTorch-CPU float32 — bench.py's CPU baseline) gives the reference's token ids too."""
+    import torch
+    from oracle.reference_as_computed import ReferenceAsComputed, padded_graphs
+    torch.set_num_threads(8)
+    for c in ("short_syn56_missing9_k4096_df2", "casp_T1082_k64000_df1", "bench256_p3_k4096_df1"):
+        n, T, cb, df, D, seed = (int(v) for v in F[c + "/meta"])
+        m = ReferenceAsComputed(P.random_params(D, seed), LEVELS[cb], df)
+        o = m.forward(padded_graphs([(F[c + "/in_positions"].astype(np.float64), F[c + "/in_flags"])], df))
+        assert np.array_equal(o["tokens"][0, :T], F[c + "/tokens_pe32"]), c
+        assert np.abs(o["bounded"][0, :T] - F[c + "/bounded_pe32"]).max() < 1e-4
