@@ -55,6 +55,31 @@ MPNN1_ALG_FLOP_PER_RES = K * 2 * MLP_FLOP + 2 * (H * 4 * H + 4 * H * H)   # 16 6
 PATH_ALG_FLOP_PER_RES = {1: 44_715_008, 4: 44_395_904}  # SURVEY §8d, whole path per residue
 
 
+T0 = time.perf_counter()
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line stays alone on stdout)."""
+    print(f"[bench {time.perf_counter() - T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def host_cores() -> int:
+    """CPU threads this process may really use: the affinity set, capped by the cgroup CPU quota
+    (a GPU box shows the whole machine's CPUs but grants a share) and by OMP_NUM_THREADS."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(-(-int(q) // int(per)))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -181,7 +206,7 @@ def casp14_end_to_end(tk):
     arc = os.path.join(ROOT, "tests", "golden", "casp14_pdbs.tar.gz")
     if not os.path.exists(arc):
         return None
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = min(16, host_cores())
     with tempfile.TemporaryDirectory() as d:
         with tarfile.open(arc) as tf:
             tf.extractall(d, members=[m for m in tf.getmembers() if m.isfile() and m.name.endswith(".pdb")])
@@ -214,13 +239,14 @@ def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok):
     from oracle import oracle as O
     from oracle.reference_as_computed import ReferenceAsComputed, padded_graphs
     from pst_amd import params as P
-    cores = len(os.sched_getaffinity(0))
+    cores = host_cores()
     out = {}
     n = min(args.cpu_sample, len(samples))
     model = ReferenceAsComputed(P.random_params(len(levels), 1234), levels, args.df)
     pf = [(s.atom37_positions, s.atom_flags()) for s in samples[:n]]
     res_n = int(sum(s.nb_residues for s in samples[:n]))
     for threads in sorted({cores, 8}, reverse=True):
+        log(f"reference-as-computed CPU baseline, {threads} threads, {n} proteins")
         torch.set_num_threads(threads)
         model.forward(padded_graphs(pf[:1], args.df))  # warm-up
         t0 = time.perf_counter()
@@ -235,6 +261,7 @@ def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok):
                                   f"graph; torch.set_num_threads({threads}) of {cores} cores available"}
     torch.set_num_threads(cores)
     m = min(args.port_sample, len(samples))
+    log(f"C-port CPU baseline, {cores} threads, {m} proteins")
     sub_R = int(off[m])
     t1 = time.perf_counter()
     otok, _ = O.tokenize_batch(blob, levels, args.df, pos[:sub_R], flags[:sub_R], off[:m + 1], n_threads=cores)
@@ -276,6 +303,7 @@ def main():
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     seen_world = dist.get_world_size() if world > 1 else 1
 
+    log(f"rank {rank}/{world}: building the synthetic workload")
     ids, samples = workload(args, rank, world)
     pos, flags, off = pack_samples(samples)
     R = int(off[-1])
@@ -287,6 +315,7 @@ def main():
     tk = Tokenizer(gpu, args.codebook, args.df, blob)
     torch.cuda.synchronize(dev)
 
+    log(f"rank {rank}: {len(samples)} proteins, {R} residues; warm-up")
     for _ in range(args.warmup):
         tk.tokenize_packed(ppos, pflags, off)
     if world > 1:
@@ -302,6 +331,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    log(f"rank {rank}: {args.steps} timed steps in {elapsed:.2f} s")
     stats = torch.tensor(times + [elapsed], dtype=torch.float64, device=red_dev)
     total_res = torch.tensor([R], dtype=torch.float64, device=red_dev)
     if world > 1:
@@ -384,9 +414,11 @@ def main():
                                       if args.df in PATH_ALG_FLOP_PER_RES else None),
     }
 
+    log("device-resident rate and stage times done")
     e2e = casp14_end_to_end(tk) if (rank == 0 and world == 1 and not args.no_e2e) else None
     cpu = cpu8 = port = exact = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("CPU baselines")
         cpu, cpu8, port, exact = cpu_baselines(args, samples, blob, levels, pos, flags, off, tok)
 
     if rank == 0:

@@ -48,12 +48,18 @@ constexpr double NODE_COOP_SIMD_FRACTION = 0.375;
 // (measured: 32 proteins 2.75 -> 2.41 ms, CASP14 1.82 -> 1.78 ms vs ~4096 waves of 2-4 blocks;
 // tools/edge_waves_sizes.sh). PST_EDGE_WAVES=n targets about n waves instead.
 constexpr int64_t SPLIT_EDGE_WAVES = 0;
-// Host-buffer calls (pst_tokenize) pipeline the atom37 H2D (≈925 B per residue, ~60 GB/s) with the
-// compute (~5 M residues/s) in up to H2D_MAX_CHUNKS protein chunks once the batch has at least
-// H2D_MIN_CHUNK_TASKS 32-residue tasks per chunk: each chunk then still fills the GPU for >= 2
-// fused rounds, and only the first chunk's copy is exposed.
+// Host-buffer calls (pst_tokenize) pipeline the atom37 H2D (≈925 B per residue, ~55 GB/s) with the
+// compute (~5 M residues/s) in protein chunks. The fused layers' time steps with
+// k = ceil(tasks / SIMDs) (use_split_schedule), so every chunk but the last holds a whole number
+// of those rounds — cutting anywhere else adds a round per chunk (bench, 8 192 tasks: an even
+// 1:4 split cost 59.2 vs 52.3 ms device-resident). The first chunk is H2D_FIRST_ROUNDS rounds
+// (its copy is the only exposed one); each next chunk is at most H2D_GROWTH times the previous
+// (the copy runs ~12x faster than the compute, so chunk k+1's copy hides under chunk k). No
+// pipeline below H2D_MIN_ROUNDS rounds in all.
 constexpr int H2D_MAX_CHUNKS = 8;
-constexpr int64_t H2D_MIN_CHUNK_TASKS = 4096;
+constexpr int64_t H2D_FIRST_ROUNDS = 2;
+constexpr int64_t H2D_GROWTH = 8;
+constexpr int64_t H2D_MIN_ROUNDS = 4;
 
 // Schedule thresholds from the environment, read once per context: -2 = not read yet, -1 = unset
 // (use the cost model), >= 0 = the override.
@@ -825,25 +831,44 @@ int pst_tokenize_device(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flag
 namespace {
 
 // Protein-boundary chunk starts [0 = c_0 < c_1 < ... < c_n = n_prot] of a pipelined host call.
-// The first chunk is a quarter of the rest's average so that little copy time is exposed; the
-// others split the remaining residues evenly.
+// Policy: whole fused rounds per chunk (see H2D_FIRST_ROUNDS). PST_H2D_CHUNKS=n forces n chunks
+// of about equal residues (the first a quarter of the others; tests of the pipeline's bits).
 std::vector<int32_t> plan_chunks(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot) {
   const int64_t R = offsets[n_prot];
-  const int64_t tasks = (R + 31) / 32;
+  // run() launches Rpad / 32 tasks, Rpad = R rounded up to 128 residues
+  auto tasks_of = [](int64_t r) { return (r + 127) / 128 * 4; };
+  const int64_t tasks = tasks_of(R);
   env_threshold(ctx->h2d_chunks, "PST_H2D_CHUNKS");
-  int n = ctx->h2d_chunks >= 1 ? (int)std::min<int64_t>(ctx->h2d_chunks, H2D_MAX_CHUNKS)
-                               : (int)std::min<int64_t>(H2D_MAX_CHUNKS, tasks / H2D_MIN_CHUNK_TASKS);
-  n = std::max(1, std::min(n, (int)n_prot));
   std::vector<int32_t> cut{0};
-  if (n > 1) {
-    // weights: first chunk 1/4 of a regular chunk
-    const double unit = (double)R / (0.25 + (n - 1));
-    double target = 0.25 * unit;
-    for (int32_t b = 1; b < n_prot && (int)cut.size() < n; ++b)
-      if ((double)offsets[b] >= target) {
-        cut.push_back(b);
-        target += unit;
-      }
+  if (ctx->h2d_chunks >= 1) {
+    const int n = std::max(1, std::min({(int)std::min<int64_t>(ctx->h2d_chunks, H2D_MAX_CHUNKS), (int)n_prot}));
+    if (n > 1) {
+      const double unit = (double)R / (0.25 + (n - 1));
+      double target = 0.25 * unit;
+      for (int32_t b = 1; b < n_prot && (int)cut.size() < n; ++b)
+        if ((double)offsets[b] >= target) {
+          cut.push_back(b);
+          target += unit;
+        }
+    }
+    cut.push_back(n_prot);
+    return cut;
+  }
+  const int64_t round = std::max<int64_t>(1, ctx->n_simds);
+  if (tasks >= H2D_MIN_ROUNDS * round) {
+    int64_t want = H2D_FIRST_ROUNDS;  // rounds in the next chunk
+    int32_t b = 0;
+    while ((int)cut.size() < H2D_MAX_CHUNKS) {
+      const int64_t r0 = offsets[b];
+      if (tasks_of(R - r0) <= want * round) break;  // the rest fits in this chunk: last chunk
+      // last protein boundary at which the chunk's tasks stay within `want` rounds
+      int32_t e = b;
+      while (e < n_prot && tasks_of(offsets[e + 1] - r0) <= want * round) ++e;
+      if (e == b) break;
+      cut.push_back(e);
+      b = e;
+      want *= H2D_GROWTH;
+    }
   }
   cut.push_back(n_prot);
   return cut;
