@@ -18,6 +18,8 @@
 #include <stdint.h>
 
 #include "pst_device.h"
+#include <utility>
+
 #include "pst_kernels.h"
 
 namespace pst {
@@ -416,6 +418,21 @@ __device__ __forceinline__ int perm_pos(int c) {
   return h * 64 + M * 16 + r;
 }
 
+// 1.0f if bit `ee` of the wave-uniform mask is set, else 0.0f, made on the scalar unit (an SGPR
+// operand of the consuming FMA; a C select would be materialised per lane)
+template <int EE>
+__device__ __forceinline__ float umask(uint32_t bits) {
+  float r;
+  asm volatile("s_bitcmp1_b32 %1, %2\n\ts_cselect_b32 %0, 1.0, 0" : "=s"(r) : "s"(bits), "I"(EE) : "scc");
+  return r;
+}
+// the two chains over the 32 edges of a block (v: this lane's channel row, edges in order)
+template <int... EE>
+__device__ __forceinline__ void seg_chains(const float (&v)[32], uint32_t mA, uint32_t mB, float& accA, float& accB,
+                                           std::integer_sequence<int, EE...>) {
+  ((accA = __builtin_fmaf(v[EE], umask<EE>(mA), accA), accB = __builtin_fmaf(v[EE], umask<EE>(mB), accB)), ...);
+}
+
 // acc = a_row + b_row (perm rows); b is streamed 4 values at a time so the sum needs one tile
 // of registers, not two
 __device__ __forceinline__ void tile_add_rows(Tile& acc, const float* __restrict__ a_row, const float* __restrict__ b_row) {
@@ -644,7 +661,7 @@ __device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t
 // ordered segment sums in registers/LDS, then the node update. No per-edge message traffic.
 template <int LAYER>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
-  __shared__ float lds_scratch[4][32 * 36];
+  __shared__ float lds_scratch[4][64 * 36];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (no waterfalls)
 #ifdef PST_XCD_REMAP
@@ -660,8 +677,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   const int64_t g0 = task * 32;
   float* scratch = lds_scratch[w];
   float* aggl = a.agg + task * 32 * 128;
-  const int c = lane & 31, part = lane >> 5;
-  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+  float carry[2] = {0.f, 0.f};  // running sums of the receiver continuing into the next block
 
   int32_t s_next = edge_sender(a, g0, lane, 0);
   for (int blk = 0; blk < 50; ++blk) {
@@ -669,45 +685,56 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     if (blk < 49) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
     edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m);
-    // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order):
-    // transpose through LDS, then each lane runs the sequential chain of its channel; lane
-    // half 0 continues the receiver that owns edge 0 of the block (rA), half 1 starts rA+1.
+    // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order). The
+    // block holds edges of two receivers: rA (block edges 0..lastA) and rA+1 (the rest).
+    // Transpose through LDS two accumulator blocks at a time, so that lane l owns channel
+    // 64·p + l of pass p and runs both receivers' sequential chains over the block's edges
+    // itself. The chain bounds are wave-uniform (no divergence, no data-dependent loops): edge
+    // ee enters chain A iff ee <= hiA and chain B iff loB <= ee <= hiB, as fmaf(v, 1, acc)
+    // (= acc + v, one rounding) or fmaf(v, 0, acc) (= acc exactly: a chain never holds -0, and
+    // messages are finite GELU outputs).
     const int rA = (32 * blk) / 50;                    // wave-uniform
     const int lastA = 50 * (rA + 1) - 1 - 32 * blk;    // block-local index of rA's last edge
     const int j0 = 32 * blk - 50 * rA;                 // slot of the block's edge 0 within rA
     const int degA = a.deg[g0 + rA];
     const int degB = rA + 1 < 32 ? a.deg[g0 + rA + 1] : 0;
-    const int hiA = min(min(lastA, 31), degA - 1 - j0);  // part 0 sums edges [0, hiA]
-    const int loB = lastA + 1;                           // part 1 sums edges [loB, hiB]
+    const int hiA = min(min(lastA, 31), degA - 1 - j0);  // chain A sums edges [0, hiA]
+    const int loB = lastA + 1;                           // chain B sums edges [loB, hiB]
     const int hiB = min(31, lastA + degB);
 #ifdef PST_EXP_NOAGG
     if (blk == 49) for (int M = 0; M < 4; ++M) aggl[M] = m.m[M][0] + m.m[M][15];
     continue;
 #endif
+    // wave-uniform edge masks of the two chains (bit ee set = edge ee enters the chain)
+    const uint32_t mA = (uint32_t)__builtin_amdgcn_readfirstlane(
+        hiA < 0 ? 0u : (hiA >= 31 ? 0xffffffffu : (1u << (hiA + 1)) - 1u));
+    const uint32_t mB = (uint32_t)__builtin_amdgcn_readfirstlane(
+        loB > hiB ? 0u : ((hiB >= 31 ? 0xffffffffu : (1u << (hiB + 1)) - 1u) & ~((1u << loB) - 1u)));
 #pragma unroll
-    for (int M = 0; M < 4; ++M) {
+    for (int p = 0; p < 2; ++p) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int ch = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        scratch[ch * 36 + (lane & 31)] = m.m[M][r];
-      }
+      for (int Mh = 0; Mh < 2; ++Mh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lc = 32 * Mh + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          scratch[lc * 36 + (lane & 31)] = m.m[2 * p + Mh][r];
+        }
       __builtin_amdgcn_wave_barrier();
-      const float* srow = scratch + c * 36;
-      float acc;
-      if (part == 0) {
-        acc = carry[M];
-        for (int ee = 0; ee <= hiA; ++ee) acc = acc + srow[ee];
-      } else {
-        acc = 0.0f;
-        for (int ee = loB; ee <= hiB; ++ee) acc = acc + srow[ee];
+      const float4* srow = reinterpret_cast<const float4*>(scratch + lane * 36);
+      float v[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 t = srow[q];
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
       }
+      float accA = carry[p], accB = 0.0f;
+      seg_chains(v, mA, mB, accA, accB, std::make_integer_sequence<int, 32>{});
       __builtin_amdgcn_wave_barrier();
-      float other = __shfl_xor(acc, 32, 64);
       if (lastA <= 31) {
-        if (part == 0) aggl[rA * 128 + perm_pos(32 * M + c)] = acc;
-        carry[M] = lastA < 31 ? other : 0.0f;
+        aggl[rA * 128 + perm_pos(64 * p + lane)] = accA;
+        carry[p] = lastA < 31 ? accB : 0.0f;
       } else {
-        carry[M] = acc;
+        carry[p] = accA;
       }
     }
   }
