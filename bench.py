@@ -203,6 +203,7 @@ def casp14_end_to_end(tk):
     import tarfile
     import tempfile
     from pst_amd._native import parse_pdb_files
+    from pst_amd.runner import save_npy_files
     arc = os.path.join(ROOT, "tests", "golden", "casp14_pdbs.tar.gz")
     if not os.path.exists(arc):
         return None
@@ -220,9 +221,9 @@ def casp14_end_to_end(tk):
             t1 = time.perf_counter()
             tok, nt, _ = tk.tokenize_packed(B.positions, B.flags, B.offsets)
             t2 = time.perf_counter()
-            for i, f in enumerate(files):
-                a = int(B.offsets[i])
-                np.save(os.path.join(out, os.path.basename(f)[:-4] + "_tokens"), tok[a:a + nt[i]].reshape(1, -1))
+            save_npy_files([os.path.join(out, os.path.basename(f)[:-4] + "_tokens") for f in files],
+                           [tok[int(B.offsets[i]):int(B.offsets[i]) + nt[i]].reshape(1, -1) for i in range(len(files))],
+                           threads=threads)
             t3 = time.perf_counter()
             R = int(B.offsets[-1])
             res = {"workload": "CASP14 31 structures (SURVEY config 2), codebook 4096, df 1", "residues": R,

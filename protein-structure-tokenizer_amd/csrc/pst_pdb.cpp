@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <atomic>
@@ -33,22 +34,6 @@
 #include "pst_residue_tables.h"
 
 namespace {
-
-struct AtomRec {
-  char name[5];
-  float xyz[3];
-  double occ;
-};
-
-struct Residue {
-  std::string resname;
-  char icode;
-  int resseq;
-  std::vector<AtomRec> atoms;
-};
-
-struct ResKey;
-struct ResKeyHash;
 
 struct Parsed {
   int status = PST_OK;
@@ -65,33 +50,50 @@ struct Field {
   int n;
   bool empty() const { return n == 0; }
   bool eq(const char* s) const { return (int)strlen(s) == n && !memcmp(p, s, n); }
-  std::string str() const { return std::string(p, n); }
 };
 
-Field field(const char* line, int len, int a, int b) {
+inline Field field(const char* line, int len, int a, int b) {
   if (b > len) b = len;
   while (a < b && (line[a] == ' ' || line[a] == '\t')) ++a;
   while (b > a && (line[b - 1] == ' ' || line[b - 1] == '\t')) --b;
   return Field{line + a, a < b ? b - a : 0};
 }
 
-bool parse_int(Field f, int* v) {
+// Python int() of a field (optional sign, decimal digits); false if malformed
+inline bool parse_int(Field f, int* v) {
   if (f.empty() || f.n > 15) return false;
-  char buf[16];
-  memcpy(buf, f.p, f.n);
-  buf[f.n] = 0;
-  errno = 0;
-  char* end = nullptr;
-  long r = strtol(buf, &end, 10);
-  if (errno || *end) return false;
-  *v = (int)r;
+  int i = 0;
+  bool neg = false;
+  if (f.p[0] == '-' || f.p[0] == '+') {
+    neg = f.p[0] == '-';
+    i = 1;
+  }
+  if (i >= f.n) return false;
+  long r = 0;
+  for (; i < f.n; ++i) {
+    const char c = f.p[i];
+    if (c < '0' || c > '9') {
+      // anything else (e.g. digit-group underscores) through strtol's stricter reading
+      char buf[16];
+      memcpy(buf, f.p, f.n);
+      buf[f.n] = 0;
+      errno = 0;
+      char* end = nullptr;
+      long x = strtol(buf, &end, 10);
+      if (errno || *end) return false;
+      *v = (int)x;
+      return true;
+    }
+    r = r * 10 + (c - '0');
+  }
+  *v = (int)(neg ? -r : r);
   return true;
 }
 
 // Python float() of a field. Fast path for the fixed-point form PDB writers emit ("-12.345"):
 // mantissa and 10^k are exact doubles, so one IEEE division is the correctly rounded value —
 // the same double strtod returns. Anything else goes through strtod.
-bool parse_double(Field f, double* v) {
+inline bool parse_double(Field f, double* v) {
   if (f.empty() || f.n > 31) return false;
   {
     int i = 0;
@@ -132,126 +134,239 @@ bool parse_double(Field f, double* v) {
   return true;
 }
 
-int restype_index(const std::string& resname) {
+// ---- atom37 name lookup: the stripped 1-4 character name packed little-endian into a uint32,
+// found in a 128-entry open-addressing table built once
+inline uint32_t pack_name(const char* p, int n) {
+  uint32_t k = 0;
+  memcpy(&k, p, n < 4 ? n : 4);
+  return k;
+}
+struct AtomTable {
+  uint32_t key[128];
+  int8_t idx[128];
+  AtomTable() {
+    memset(key, 0, sizeof(key));
+    memset(idx, -1, sizeof(idx));
+    for (int a = 0; a < pst::kAtomTypes; ++a) {
+      const uint32_t k = pack_name(pst::kAtomNames[a], (int)strlen(pst::kAtomNames[a]));
+      uint32_t h = (k * 2654435761u) >> 25;
+      while (idx[h] >= 0) h = (h + 1) & 127;
+      key[h] = k;
+      idx[h] = (int8_t)a;
+    }
+  }
+  int find(uint32_t k) const {
+    for (uint32_t h = (k * 2654435761u) >> 25;; h = (h + 1) & 127) {
+      if (idx[h] < 0) return -1;
+      if (key[h] == k) return idx[h];
+    }
+  }
+};
+const AtomTable& atom_table() {
+  static const AtomTable t;
+  return t;
+}
+
+int restype_index(Field resname) {
   for (int r = 0; r < 20; ++r)
-    if (resname == pst::kResName3[r]) return r;
+    if (resname.eq(pst::kResName3[r])) return r;
   return 20;
 }
 
-struct ResKey {
-  std::string het;
+// One residue as Bio builds it, reduced to what the output keeps: its atom37 slots. A repeated
+// atom name keeps the first record unless an altloc record has a strictly higher occupancy;
+// atoms outside atom37 never reach the output, so they are not stored at all.
+struct Res {
   int resseq;
   char icode;
-  bool operator==(const ResKey& o) const { return resseq == o.resseq && icode == o.icode && het == o.het; }
-};
-struct ResKeyHash {
-  size_t operator()(const ResKey& k) const {
-    return std::hash<std::string>()(k.het) ^ ((size_t)k.resseq * 131u) ^ ((size_t)(unsigned char)k.icode << 20);
-  }
+  uint8_t restype;
+  uint64_t present;  // bit a: atom37 slot a filled
+  float xyz[pst::kAtomTypes][3];
+  double occ[pst::kAtomTypes];
 };
 
 struct Chain {
   char id;
-  std::vector<Residue> residues;
-  std::vector<ResKey> keys;
-  std::unordered_map<ResKey, int, ResKeyHash> index;
+  uint64_t last_key;
+  int last_res;
+  std::vector<int> residues;                // residue ids in order of first appearance
+  std::unordered_map<uint64_t, int> index;  // key -> residue id
 };
 
-int atom_index(const char* name) {
-  for (int a = 0; a < pst::kAtomTypes; ++a)
-    if (!strcmp(name, pst::kAtomNames[a])) return a;
-  return -1;
+// Residue keys (het flag, resseq, icode[, resname]) are packed into 64 bits in assemble():
+// het 0 = ATOM " ", 1 = water "W", 2 = "H_<resname>" (resname in bits 34..57).
+
+// ---- pass 1 (parallel over line-aligned chunks of a file): each line's record, fields parsed
+enum RecKind : uint8_t { R_ATOM, R_HETATM, R_MODEL, R_ENDMDL, R_STOP, R_BAD_COORD, R_BAD_OCC };
+
+struct Rec {
+  uint8_t kind;
+  char altloc, chain, icode;
+  int8_t atom;      // atom37 index or -1
+  uint8_t restype;  // 0..20
+  uint8_t het;      // 0 ATOM, 1 water, 2 other HETATM
+  int32_t resseq;
+  uint32_t resname;  // packed (het == 2 keys only)
+  float xyz[3];
+  double occ;
+  uint32_t line;     // byte offset of the line (error messages)
+};
+
+inline int line_len_at(const char* text, size_t len, size_t p, size_t* next) {
+  const char* line = text + p;
+  const char* nl = (const char*)memchr(line, '\n', len - p);
+  size_t q = nl ? (size_t)(nl - text) : len;
+  const char* cr = (const char*)memchr(line, '\r', q - p);  // a lone '\r' ends a line too
+  if (cr) q = (size_t)(cr - text);
+  *next = (q + 1 < len && text[q] == '\r' && text[q + 1] == '\n') ? q + 2 : q + 1;  // \n, \r\n or \r
+  return (int)(q - p);
 }
 
-void parse_one(const char* text, size_t len, char chain_filter, Parsed* out) {
-  int models = 0;
-  bool seen_atom_before_model = false, in_first = true, started = false;
-  std::vector<Chain> chains;
-  size_t p = 0;
-  while (p < len) {
-    size_t q = p;
-    while (q < len && text[q] != '\n' && text[q] != '\r') ++q;
+// Records of the lines starting in [p0, p1) (p0 at a line start). Only the records Bio's reader
+// acts on are kept: ATOM/HETATM (fields parsed; a malformed one becomes R_BAD_* and raises only if
+// pass 2 reaches it), MODEL, ENDMDL and the CONECT / "END   " stop records.
+void scan_chunk(const char* text, size_t len, size_t p0, size_t p1, std::vector<Rec>* out) {
+  const AtomTable& T = atom_table();
+  out->reserve(out->size() + (p1 - p0) / 80 + 4);
+  size_t p = p0;
+  while (p < p1) {
+    size_t next;
     const char* line = text + p;
-    const int ll = (int)(q - p);
-    p = (q + 1 < len && text[q] == '\r' && text[q + 1] == '\n') ? q + 2 : q + 1;  // \n, \r\n or \r
-    // Bio names a record by its exact first 6 columns; its header ends at the first ATOM/HETATM/
-    // MODEL record and the atomic data at the first CONECT or "END   " record
-    auto rec = [&](const char* name6) { return ll >= 6 && !memcmp(line, name6, 6); };
-    const bool is_atom = rec("ATOM  "), is_het = rec("HETATM"), is_model = rec("MODEL ");
-    if (!started) {
-      if (!is_atom && !is_het && !is_model) continue;
-      started = true;
-    }
-    if (rec("CONECT") || rec("END   ")) break;
-    if (is_model) {
-      ++models;
-      in_first = models == 1;
+    const int ll = line_len_at(text, len, p, &next);
+    const uint32_t at = (uint32_t)p;
+    p = next;
+    if (ll < 6) continue;  // no 6-column record name (a bare "END" is not Bio's "END   ")
+    Rec r;
+    r.line = at;
+    const bool is_atom = !memcmp(line, "ATOM  ", 6), is_het = !is_atom && !memcmp(line, "HETATM", 6);
+    if (!is_atom && !is_het) {
+      if (!memcmp(line, "MODEL ", 6)) r.kind = R_MODEL;
+      else if (!memcmp(line, "ENDMDL", 6)) r.kind = R_ENDMDL;
+      else if (!memcmp(line, "CONECT", 6) || !memcmp(line, "END   ", 6)) r.kind = R_STOP;
+      else continue;  // any other record: Bio skips it
+      out->push_back(r);
       continue;
     }
-    if (rec("ENDMDL")) {
-      in_first = false;
-      continue;
-    }
-    if (!is_atom && !is_het) continue;
-    if (models == 0) seen_atom_before_model = true;
-    if (!in_first && models > 0) continue;
+    r.kind = is_atom ? R_ATOM : R_HETATM;
     const Field name = field(line, ll, 12, 16);
-    const char altloc = 16 < ll ? line[16] : ' ';
+    r.altloc = 16 < ll ? line[16] : ' ';
     const Field resname = field(line, ll, 17, 20);
-    const char chain = 21 < ll ? line[21] : ' ';
-    const char icode = 26 < ll ? line[26] : ' ';
+    r.chain = 21 < ll ? line[21] : ' ';
+    r.icode = 26 < ll ? line[26] : ' ';
     int resseq;
     double x = 0.0, y = 0.0, z = 0.0, occ = 0.0;
     if (!parse_int(field(line, ll, 22, 26), &resseq) || !parse_double(field(line, ll, 30, 38), &x) ||
         !parse_double(field(line, ll, 38, 46), &y) || !parse_double(field(line, ll, 46, 54), &z)) {
-      out->status = PST_E_INVALID;
-      out->error = "malformed ATOM/HETATM record: " + std::string(line, std::min(ll, 80));
-      return;
+      r.kind = R_BAD_COORD;
+      out->push_back(r);
+      continue;
     }
     const Field occ_s = field(line, ll, 54, 60);
     if (!occ_s.empty() && !parse_double(occ_s, &occ)) {
-      out->status = PST_E_INVALID;
-      out->error = "malformed occupancy: " + std::string(line, std::min(ll, 80));
-      return;
+      r.kind = R_BAD_OCC;
+      out->push_back(r);
+      continue;
     }
-    ResKey key{" ", resseq, icode};
-    if (is_het) key.het = (resname.eq("HOH") || resname.eq("WAT")) ? std::string("W") : "H_" + resname.str();
-    Chain* ch = nullptr;
-    for (auto& c : chains)
-      if (c.id == chain) ch = &c;
-    if (!ch) {
-      chains.push_back(Chain{chain, {}, {}, {}});
-      ch = &chains.back();
-    }
-    int ri = -1;
-    if (!ch->keys.empty() && ch->keys.back() == key) {  // records of a residue are contiguous
-      ri = (int)ch->keys.size() - 1;
-    } else {
-      auto it = ch->index.find(key);
-      if (it == ch->index.end()) {
-        ri = (int)ch->residues.size();
-        ch->index.emplace(key, ri);
-        ch->keys.push_back(key);
-        ch->residues.push_back(Residue{resname.str(), icode, resseq, {}});
+    r.resseq = resseq;
+    r.het = is_het ? ((resname.eq("HOH") || resname.eq("WAT")) ? 1 : 2) : 0;
+    r.resname = pack_name(resname.p, resname.n);
+    r.restype = (uint8_t)restype_index(resname);
+    r.atom = (int8_t)(name.n >= 1 && name.n <= 4 ? T.find(pack_name(name.p, name.n)) : -1);
+    r.xyz[0] = (float)x;
+    r.xyz[1] = (float)y;
+    r.xyz[2] = (float)z;
+    r.occ = occ;
+    out->push_back(r);
+  }
+}
+
+// ---- pass 2 (sequential per file): Bio's reading order over the records of all chunks
+void assemble(const char* text, size_t len, const std::vector<std::vector<Rec>>& chunks, char chain_filter,
+              Parsed* out) {
+  int models = 0;
+  bool seen_atom_before_model = false, in_first = true, started = false;
+  std::vector<Chain> chains;
+  std::vector<Res> res;
+  res.reserve(len / 600 + 16);  // ~8 atom records of ~81 bytes per residue
+  auto line_text = [&](uint32_t at) {
+    size_t next;
+    const int ll = line_len_at(text, len, at, &next);
+    return std::string(text + at, std::min(ll, 80));
+  };
+  bool stop = false;
+  for (const auto& recs : chunks) {
+    for (const Rec& r : recs) {
+      // Bio's header ends at the first ATOM/HETATM/MODEL record and the atomic data at the first
+      // CONECT or "END   " record
+      if (r.kind == R_MODEL) {
+        started = true;
+        ++models;
+        in_first = models == 1;
+        continue;
+      }
+      if (!started && r.kind != R_ATOM && r.kind != R_HETATM && r.kind != R_BAD_COORD && r.kind != R_BAD_OCC)
+        continue;
+      if (r.kind == R_STOP) {
+        stop = true;
+        break;
+      }
+      if (r.kind == R_ENDMDL) {
+        in_first = false;
+        continue;
+      }
+      started = true;
+      if (models == 0) seen_atom_before_model = true;
+      if (!in_first && models > 0) continue;
+      if (r.kind == R_BAD_COORD || r.kind == R_BAD_OCC) {
+        out->status = PST_E_INVALID;
+        out->error = (r.kind == R_BAD_COORD ? "malformed ATOM/HETATM record: " : "malformed occupancy: ") +
+                     line_text(r.line);
+        return;
+      }
+      const uint64_t key = (uint64_t)r.het | ((uint64_t)(uint32_t)(r.resseq + 1024) & 0xffffffu) << 2 |
+                           (uint64_t)(unsigned char)r.icode << 26 |
+                           (r.het == 2 ? (uint64_t)r.resname << 34 : 0ull);
+      Chain* ch = nullptr;
+      for (auto& c : chains)
+        if (c.id == r.chain) ch = &c;
+      if (!ch) {
+        chains.push_back(Chain{r.chain, ~0ull, -1, {}, {}});
+        ch = &chains.back();
+      }
+      int ri;
+      if (ch->last_res >= 0 && ch->last_key == key) {  // records of a residue are contiguous
+        ri = ch->last_res;
       } else {
-        ri = it->second;
+        auto it = ch->index.find(key);
+        if (it == ch->index.end()) {
+          ri = (int)res.size();
+          res.emplace_back();
+          Res& nr = res.back();
+          nr.resseq = r.resseq;
+          nr.icode = r.icode;
+          nr.restype = r.restype;
+          nr.present = 0;
+          ch->index.emplace(key, ri);
+          ch->residues.push_back(ri);
+        } else {
+          ri = it->second;
+        }
+        ch->last_key = key;
+        ch->last_res = ri;
+      }
+      const int a = r.atom;
+      if (a < 0) continue;  // not an atom37 atom: never reaches the output
+      Res& x = res[ri];
+      const uint64_t bit = 1ull << a;
+      if (!(x.present & bit) || (r.altloc != ' ' && r.occ > x.occ[a])) {
+        x.present |= bit;
+        x.xyz[a][0] = r.xyz[0];
+        x.xyz[a][1] = r.xyz[1];
+        x.xyz[a][2] = r.xyz[2];
+        x.occ[a] = r.occ;
       }
     }
-    Residue& res = ch->residues[ri];
-    AtomRec a{};
-    memcpy(a.name, name.p, std::min(name.n, 4));
-    a.xyz[0] = (float)x;
-    a.xyz[1] = (float)y;
-    a.xyz[2] = (float)z;
-    a.occ = occ;
-    AtomRec* prev = nullptr;
-    for (auto& r : res.atoms)
-      if (!strcmp(r.name, a.name)) prev = &r;
-    if (!prev) {
-      res.atoms.push_back(a);
-    } else if (altloc != ' ' && occ > prev->occ) {
-      *prev = a;
-    }
+    if (stop) break;
   }
   const int n_models = (models || seen_atom_before_model) ? std::max(models, 1) : 0;
   if (n_models != 1) {
@@ -259,35 +374,56 @@ void parse_one(const char* text, size_t len, char chain_filter, Parsed* out) {
     out->error = "Only single model PDBs are supported. Found " + std::to_string(n_models) + " models.";
     return;
   }
+  size_t n_keep = 0;
   for (const auto& ch : chains) {
     if (chain_filter && ch.id != chain_filter) continue;
-    for (const auto& res : ch.residues) {
-      if (res.icode != ' ') {
+    for (int ri : ch.residues) {
+      const Res& r = res[ri];
+      if (r.icode != ' ') {
         out->status = PST_E_INVALID;
         out->error = std::string("PDB contains an insertion code at chain ") + ch.id + " and residue index " +
-                     std::to_string(res.resseq) + ". These are not supported.";
+                     std::to_string(r.resseq) + ". These are not supported.";
         return;
       }
-      double pos[pst::kAtomTypes][3] = {};
-      uint8_t mask[pst::kAtomTypes] = {};
-      int n_atoms = 0;
-      for (const auto& a : res.atoms) {
-        const int ai = atom_index(a.name);
-        if (ai < 0) continue;
-        for (int d = 0; d < 3; ++d) pos[ai][d] = (double)a.xyz[d];
-        if (!mask[ai]) ++n_atoms;
-        mask[ai] = 1;
-      }
-      if (n_atoms == 0) continue;
-      const int rt = restype_index(res.resname);
-      out->aatype.push_back((uint8_t)rt);
-      for (int ai = 0; ai < pst::kAtomTypes; ++ai) {
-        for (int d = 0; d < 3; ++d) out->pos.push_back(pos[ai][d]);
-        out->flags.push_back((uint8_t)(mask[ai] | (pst::kResAtomExists[rt][ai] << 1)));
-      }
-      ++out->n;
+      n_keep += r.present != 0;
     }
   }
+  out->pos.resize(n_keep * pst::kAtomTypes * 3);
+  out->flags.resize(n_keep * pst::kAtomTypes);
+  out->aatype.resize(n_keep);
+  size_t k = 0;
+  for (const auto& ch : chains) {
+    if (chain_filter && ch.id != chain_filter) continue;
+    for (int ri : ch.residues) {
+      const Res& r = res[ri];
+      if (!r.present) continue;  // no atom37 atom: skipped (protein_structure_sample.py:228-230)
+      double* pos = out->pos.data() + k * pst::kAtomTypes * 3;
+      uint8_t* fl = out->flags.data() + k * pst::kAtomTypes;
+      for (int a = 0; a < pst::kAtomTypes; ++a) {
+        const bool has = (r.present >> a) & 1;
+        pos[3 * a + 0] = has ? (double)r.xyz[a][0] : 0.0;
+        pos[3 * a + 1] = has ? (double)r.xyz[a][1] : 0.0;
+        pos[3 * a + 2] = has ? (double)r.xyz[a][2] : 0.0;
+        fl[a] = (uint8_t)((has ? 1 : 0) | (pst::kResAtomExists[r.restype][a] << 1));
+      }
+      out->aatype[k] = r.restype;
+      ++k;
+    }
+  }
+  out->n = (int64_t)n_keep;
+}
+
+// Line-aligned chunk starts of a text: about `target` bytes each, cut after a '\n'
+std::vector<size_t> chunk_starts(const char* text, size_t len, size_t target) {
+  std::vector<size_t> st{0};
+  size_t p = target;
+  while (p < len) {
+    const char* nl = (const char*)memchr(text + p, '\n', len - p);
+    if (!nl || (size_t)(nl - text) + 1 >= len) break;
+    st.push_back((size_t)(nl - text) + 1);
+    p = st.back() + target;
+  }
+  return st;
 }
 
 bool read_file(const char* path, std::string* s, std::string* err) {
@@ -317,17 +453,55 @@ struct pst_pdb_batch {
 
 namespace {
 
-int run_pool(int32_t n, int32_t n_threads, const std::function<void(int)>& fn) {
+// fn(i) for i < n on n_threads threads, largest `size` first (the biggest file bounds the call)
+int run_pool(int32_t n, int32_t n_threads, const std::function<size_t(int)>& size, const std::function<void(int)>& fn) {
   int T = std::max(1, std::min<int>(n_threads > 0 ? n_threads : 1, n));
+  std::vector<int> order(n);
+  std::vector<size_t> sz(n);
+  for (int i = 0; i < n; ++i) {
+    order[i] = i;
+    sz[i] = size(i);
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return sz[a] > sz[b]; });
   std::atomic<int> next(0);
   auto worker = [&]() {
-    for (int i = next++; i < n; i = next++) fn(i);
+    for (int i = next++; i < n; i = next++) fn(order[i]);
   };
   std::vector<std::thread> th;
   for (int t = 1; t < T; ++t) th.emplace_back(worker);
   worker();
   for (auto& t : th) t.join();
   return PST_OK;
+}
+
+// Chunk size of pass 1: a 320 KB PDB file (the largest CASP14 one) splits into ~7 chunks
+constexpr size_t kScanChunk = 48 << 10;
+
+// Both passes over the n texts of a batch (items already marked failed are skipped): pass 1 over
+// all chunks of all texts at once, then pass 2 per text, each on the thread pool
+void parse_texts(int32_t n, const char* const* texts, const size_t* lens, char chain_id, int32_t n_threads,
+                 std::vector<Parsed>& items) {
+  std::vector<std::vector<size_t>> starts(n);
+  std::vector<std::vector<std::vector<Rec>>> recs(n);
+  std::vector<std::pair<int, int>> tasks;
+  for (int32_t i = 0; i < n; ++i) {
+    if (items[i].status != PST_OK) continue;
+    starts[i] = chunk_starts(texts[i], lens[i], kScanChunk);
+    recs[i].resize(starts[i].size());
+    for (int c = 0; c < (int)starts[i].size(); ++c) tasks.emplace_back(i, c);
+  }
+  auto chunk_end = [&](int i, int c) { return c + 1 < (int)starts[i].size() ? starts[i][c + 1] : lens[i]; };
+  run_pool((int32_t)tasks.size(), n_threads,
+           [&](int t) { return chunk_end(tasks[t].first, tasks[t].second) - starts[tasks[t].first][tasks[t].second]; },
+           [&](int t) {
+             const int i = tasks[t].first, c = tasks[t].second;
+             scan_chunk(texts[i], lens[i], starts[i][c], chunk_end(i, c), &recs[i][c]);
+           });
+  run_pool(n, n_threads, [&](int i) { return lens[i]; }, [&](int i) {
+    if (items[i].status != PST_OK) return;
+    assemble(texts[i], lens[i], recs[i], chain_id, &items[i]);
+    std::vector<std::vector<Rec>>().swap(recs[i]);
+  });
 }
 
 }  // namespace
@@ -339,7 +513,7 @@ int pst_pdb_parse_strings(const char* const* texts, const size_t* lens, int32_t 
   if (!out || n < 0 || (n > 0 && (!texts || !lens))) return PST_E_INVALID;
   auto* b = new pst_pdb_batch();
   b->items.resize(n);
-  run_pool(n, n_threads, [&](int i) { parse_one(texts[i], lens[i], chain_id, &b->items[i]); });
+  parse_texts(n, texts, lens, chain_id, n_threads, b->items);
   *out = b;
   return PST_OK;
 }
@@ -348,15 +522,24 @@ int pst_pdb_parse_files(const char* const* paths, int32_t n, char chain_id, int3
   if (!out || n < 0 || (n > 0 && !paths)) return PST_E_INVALID;
   auto* b = new pst_pdb_batch();
   b->items.resize(n);
+  std::vector<std::string> text(n);
   run_pool(n, n_threads, [&](int i) {
-    std::string s, err;
-    if (!read_file(paths[i], &s, &err)) {
+    struct stat st;
+    return stat(paths[i], &st) == 0 ? (size_t)st.st_size : (size_t)0;
+  }, [&](int i) {
+    std::string err;
+    if (!read_file(paths[i], &text[i], &err)) {
       b->items[i].status = PST_E_INVALID;
       b->items[i].error = err;
-      return;
     }
-    parse_one(s.data(), s.size(), chain_id, &b->items[i]);
   });
+  std::vector<const char*> tp(n);
+  std::vector<size_t> tl(n);
+  for (int32_t i = 0; i < n; ++i) {
+    tp[i] = text[i].data();
+    tl[i] = text[i].size();
+  }
+  parse_texts(n, tp.data(), tl.data(), chain_id, n_threads, b->items);
   *out = b;
   return PST_OK;
 }
@@ -373,17 +556,21 @@ int pst_pdb_batch_sizes(const pst_pdb_batch* b, int32_t* n, int64_t* n_residues)
 int pst_pdb_batch_copy(const pst_pdb_batch* b, double* positions, uint8_t* flags, uint8_t* aatype, int64_t* offsets,
                        int32_t* status) {
   if (!b) return PST_E_INVALID;
-  int64_t r = 0;
-  for (size_t i = 0; i < b->items.size(); ++i) {
+  const int32_t n = (int32_t)b->items.size();
+  std::vector<int64_t> off(n + 1, 0);
+  for (int32_t i = 0; i < n; ++i) off[i + 1] = off[i] + b->items[i].n;
+  if (offsets) memcpy(offsets, off.data(), sizeof(int64_t) * (n + 1));
+  for (int32_t i = 0; i < n; ++i)
+    if (status) status[i] = b->items[i].status;
+  // the copies (~925 B per residue) on a few threads once there are megabytes of them
+  const int threads = off[n] * 925 > (4 << 20) ? 8 : 1;
+  run_pool(n, threads, [&](int i) { return (size_t)b->items[i].n; }, [&](int i) {
     const Parsed& it = b->items[i];
-    if (offsets) offsets[i] = r;
-    if (status) status[i] = it.status;
+    const int64_t r = off[i];
     if (positions && it.n) memcpy(positions + r * 111, it.pos.data(), sizeof(double) * 111 * it.n);
     if (flags && it.n) memcpy(flags + r * 37, it.flags.data(), 37 * it.n);
     if (aatype && it.n) memcpy(aatype + r, it.aatype.data(), it.n);
-    r += it.n;
-  }
-  if (offsets) offsets[b->items.size()] = r;
+  });
   return PST_OK;
 }
 

@@ -158,9 +158,10 @@ def _collect_pdb(h) -> PdbBatch:
         r = ctypes.c_int64()
         L.pst_pdb_batch_sizes(h, ctypes.byref(n), ctypes.byref(r))
         n, r = n.value, r.value
-        pos = np.zeros((r, 37, 3), np.float64)
-        fl = np.zeros((r, 37), np.uint8)
-        aa = np.zeros(r, np.uint8)
+        # every element is written by pst_pdb_batch_copy (absent atoms as 0.0)
+        pos = np.empty((r, 37, 3), np.float64)
+        fl = np.empty((r, 37), np.uint8)
+        aa = np.empty(r, np.uint8)
         off = np.zeros(n + 1, np.int64)
         st = np.zeros(n, np.int32)
         L.pst_pdb_batch_copy(h, _ptr(pos), _ptr(fl), _ptr(aa), _ptr(off), _ptr(st))

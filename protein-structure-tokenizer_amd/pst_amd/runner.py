@@ -38,6 +38,47 @@ from .sample import ProteinStructureSample
 
 
 PARSE_THREADS = int(os.environ.get("PST_PARSE_THREADS", "8"))
+WRITE_THREADS = int(os.environ.get("PST_WRITE_THREADS", "8"))
+
+
+def npy_bytes(a: np.ndarray) -> bytes:
+    """The bytes `np.save` writes for a C-contiguous array of a little-endian numeric dtype
+    (format 1.0, header padded to a multiple of 64): built directly, without np.save's
+    per-call file-object machinery (tests/test_host.py checks byte equality with np.save)."""
+    a = np.ascontiguousarray(a)
+    shape = "(" + "".join(f"{d}, " for d in a.shape)[:-2] + ("," if a.ndim == 1 else "") + ")"
+    d = "{'descr': '%s', 'fortran_order': False, 'shape': %s, }" % (a.dtype.str, shape)
+    n = 10 + len(d) + 1
+    d = d + " " * ((64 - n % 64) % 64) + "\n"
+    return b"\x93NUMPY\x01\x00" + len(d).to_bytes(2, "little") + d.encode("latin1") + a.tobytes()
+
+
+def save_npy_files(paths: Sequence[str], arrays: Sequence[np.ndarray], threads: int = WRITE_THREADS) -> None:
+    """np.save(path, array) for every pair (path gets ".npy" appended as np.save does), the
+    file writes spread over `threads` threads (each write releases the GIL)."""
+    last = {p: i for i, p in enumerate(paths)}  # a path listed twice: its last array wins, as with np.save
+    todo = sorted(last.values())
+
+    def one(i):
+        p = paths[i] if paths[i].endswith(".npy") else paths[i] + ".npy"
+        with open(p, "wb") as fh:
+            fh.write(npy_bytes(arrays[i]))
+    if threads <= 1 or len(todo) < 4:
+        for i in todo:
+            one(i)
+        return
+    list(_writer_pool(threads).map(one, todo))
+
+
+_WRITERS: Dict[int, _cf.ThreadPoolExecutor] = {}
+
+
+def _writer_pool(threads: int) -> _cf.ThreadPoolExecutor:
+    """One long-lived pool per size: starting threads per call costs more than the writes."""
+    ex = _WRITERS.get(threads)
+    if ex is None:
+        ex = _WRITERS[threads] = _cf.ThreadPoolExecutor(max_workers=threads, thread_name_prefix="pst-npy")
+    return ex
 
 
 # ------------------------------------------------------------------------------- graph inputs
@@ -373,10 +414,13 @@ class InferenceRunner:
                 out = quantize(model_params, random_key, batched)
                 tokens = out["tokens"].reshape(effective_batch_size, -1)
                 n_tok = out["n_tokens"].reshape(effective_batch_size)
+                names, arrays = [], []
                 for seq_id in range(effective_batch_size):
                     token_array = tokens[seq_id].reshape(1, -1)[:, :n_tok[seq_id]]
                     filename = os.path.basename(files[seq_id]).split(".pdb")[0]
-                    np.save(os.path.join(token_save_path, filename + "_tokens"), token_array)
+                    names.append(os.path.join(token_save_path, filename + "_tokens"))
+                    arrays.append(token_array)
+                save_npy_files(names, arrays)  # = np.save per file (inference_runner.py:313-321)
                 if logger is not None:
                     logger.info(f"Took {time.perf_counter() - start_time}s to tokenize")
 

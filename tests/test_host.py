@@ -341,3 +341,56 @@ def test_make_graph_no_backbone_raises_like_reference(tmp_path):
     with pytest.raises(ValueError, match="need at least one array"):
         runner.make_graph_from_pdb(p, num_neighbor=50, downsampling_ratio=1, residue_loc_is_alphac=True,
                                    padding_num_residue=512)
+
+
+def test_npy_writer_bytes_equal_np_save(tmp_path):
+    """runner.save_npy_files (the CLI's token writer) writes exactly np.save's bytes."""
+    import io
+    from pst_amd.runner import npy_bytes, save_npy_files
+    arrs = [np.arange(391, dtype=np.uint32).reshape(1, -1), np.zeros((1, 0), np.uint32),
+            np.arange(5, dtype=np.float64), np.ones((3, 4, 5), np.float32)]
+    for a in arrs:
+        b = io.BytesIO()
+        np.save(b, a)
+        assert b.getvalue() == npy_bytes(a), a.shape
+    paths = [str(tmp_path / f"t{i}") for i in range(len(arrs))] + [str(tmp_path / "t0")]
+    save_npy_files(paths, arrs + [arrs[0] + 1], threads=4)
+    assert np.array_equal(np.load(str(tmp_path / "t0.npy")), arrs[0] + 1)
+    for i in range(1, len(arrs)):
+        assert np.array_equal(np.load(paths[i] + ".npy"), arrs[i])
+
+
+def _big_variants():
+    """Texts well above the native parser's 48 KB scan chunk, with the record sequences that
+    matter placed deep inside (so they fall in later chunks or straddle chunk boundaries)."""
+    lines = pdb.to_pdb_string(synthetic.synthetic_protein(400, 11)).splitlines()[:-1]  # drop END
+    n = len(lines)
+    k = (2 * n) // 3
+    bad = lines[k][:30] + "   x.abc" + lines[k][38:]
+    alt = [_atom(90000 + i, "CB", "ALA", "A", 1, 1.0 * i, 2.0, 3.0, occ=o, altloc=a)
+           for i, (o, a) in enumerate(((0.2, "A"), (0.6, "B"), (0.9, " "), (0.7, "C")))]
+    return {
+        "plain": "\n".join(lines + ["END"]),
+        "conect_late": "\n".join(lines[:k] + ["CONECT    1    2"] + lines[k:]),
+        "malformed_after_conect": "\n".join(lines[:k] + ["CONECT    1    2", bad] + lines[k:]),
+        "malformed_late": "\n".join(lines[:k] + [bad] + lines[k:]),
+        "second_model_late": "\n".join(["MODEL        1"] + lines[:k] + ["ENDMDL", "MODEL        2"] + lines[k:]),
+        "altloc_late": "\n".join(lines[:k] + alt + lines[k:]),
+        "crlf": "\r\n".join(lines),
+    }
+
+
+@pytest.mark.parametrize("case", sorted(_big_variants()))
+def test_native_parser_multichunk_matches_restatement(case):
+    """The native parser scans big files in parallel line-aligned chunks and replays the records
+    in order: every text above splits into >= 3 chunks and must read as the restatement does."""
+    txt = _big_variants()[case]
+    assert len(txt) > 2 * 48 * 1024  # >= 3 chunks
+    if case == "malformed_late":  # both raise ValueError; the messages differ by design
+        from pst_amd import _native
+        with pytest.raises(ValueError):
+            pdb.protein_structure_from_pdb_string(txt)
+        nat = _native.parse_pdb_strings([txt], n_threads=4)
+        assert nat.status[0] != 0 and nat.errors[0].startswith("malformed ATOM/HETATM record")
+        return
+    _both(txt)
