@@ -11,16 +11,15 @@
 //   → [PE(j−i) | pair] → Linear → Transition = z                    sequence_decoder.py, modules.py:639-740
 //   structure module: 8 fold iterations (IPA with pair bias and point attention, transitions,
 //   quaternion backbone update, backbone torsions → frames → atom14 → atom37)        folding.py
-// Kernels are plain fp32 (VALU fma chains, LDS-tiled GEMM); this path is not the benchmarked one.
+// Kernels are plain fp32 (no bitwise claim): the pair chain as one fused f32-MFMA kernel
+// (k_pair_fused), per-node GEMMs on the in-tree f32-MFMA k_gemm_mfma (no library GEMM), the rest
+// hand-written (LayerNorm, gated cross-attention, IPA, frame geometry).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <cmath>
 #include <string>
 #include <vector>
-
-#include <hipblaslt/hipblaslt.h>
-#include <rocblas/rocblas.h>
 
 #include <array>
 #include <map>
@@ -103,18 +102,102 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ X, int l
   }
 }
 
-// epilogue of a library GEMM: y = act(y + b); a wave per row, 4 rows per block
-__global__ __launch_bounds__(256) void k_bias_act(float* __restrict__ Y, int ldy, const float* __restrict__ b,
-                                                  int64_t M, int N, int flags) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= M) return;
-  float* y = Y + r * ldy;
-  for (int c = threadIdx.x & 63; c < N; c += 64) {
-    float v = y[c];
-    if (b) v = v + b[c];
-    if (flags & F_RELU_OUT) v = v > 0.0f ? v : 0.0f;
-    if (flags & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
-    y[c] = v;
+// The same GEMM on f32 MFMA (v_mfma_f32_32x32x2_f32), split over K: a block owns one
+// 32 × (32·NACC) output tile and its SLICES waves take consecutive K ranges of `kslice` (a
+// multiple of 4), so a wave's dependent MFMA chain is K / SLICES / 2 long instead of K / 2 — these
+// GEMMs have a few thousand rows at most, and their time is that chain and the re-reads of X (one
+// per column tile: NACC accumulators per wave cut them), not MFMA throughput. A fragments come
+// straight from X rows (one float4 = two k-steps of a lane: k = 4s + h and 4s + 2 + h for lane
+// half h), B fragments from W columns (coalesced 128-byte rows); act_in is applied on load. The
+// slices' partial tiles are summed in slice order through LDS, then bias / activation /
+// accumulation. Needs K % 4 == 0, ldx % 4 == 0 and a 16-byte aligned X (gemm_any checks; k_gemm
+// otherwise).
+template <int SLICES, int NACC>
+__global__ __launch_bounds__(64 * SLICES) void k_gemm_mfma(const float* __restrict__ X, int ldx,
+                                                           const float* __restrict__ W, int ldw,
+                                                           const float* __restrict__ b, float* __restrict__ Y,
+                                                           int ldy, int M, int N, int K, int flags, int kslice) {
+  __shared__ float part[SLICES][16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row0 = blockIdx.y * 32, col0 = blockIdx.x * 32 * NACC;
+  const int i = lane & 31, h = lane >> 5;
+  const float* xr = X + (int64_t)min(row0 + i, M - 1) * ldx;  // rows past M: clamped, not stored
+  bool cv[NACC];
+  const float* wc[NACC];
+#pragma unroll
+  for (int t = 0; t < NACC; ++t) {
+    const int c = col0 + 32 * t + i;
+    cv[t] = c < N;
+    wc[t] = W + (cv[t] ? c : 0) + (int64_t)h * ldw;
+  }
+  const bool relu_in = flags & F_RELU_IN;
+  const int k0 = w * kslice, k1 = min(K, k0 + kslice);
+  f32x16 acc[NACC];
+#pragma unroll
+  for (int t = 0; t < NACC; ++t) acc[t] = f32x16{};
+  int k = k0;
+  for (; k + 8 <= k1; k += 8) {  // 2 fragment groups per trip, loads ahead of their MFMAs
+    float4 xa[2];
+    float bw[2][NACC][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      xa[u] = *reinterpret_cast<const float4*>(xr + k + 4 * u);
+#pragma unroll
+      for (int t = 0; t < NACC; ++t) {
+        bw[u][t][0] = cv[t] ? wc[t][(int64_t)(k + 4 * u) * ldw] : 0.0f;
+        bw[u][t][1] = cv[t] ? wc[t][(int64_t)(k + 4 * u + 2) * ldw] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float4 x = xa[u];
+      if (relu_in) {
+        x.x = x.x > 0.0f ? x.x : 0.0f;
+        x.y = x.y > 0.0f ? x.y : 0.0f;
+        x.z = x.z > 0.0f ? x.z : 0.0f;
+        x.w = x.w > 0.0f ? x.w : 0.0f;
+      }
+#pragma unroll
+      for (int t = 0; t < NACC; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? x.y : x.x, bw[u][t][0], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NACC; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? x.w : x.z, bw[u][t][1], acc[t], 0, 0, 0);
+    }
+  }
+  for (; k < k1; k += 4) {
+    float4 x = *reinterpret_cast<const float4*>(xr + k);
+    if (relu_in) {
+      x.x = x.x > 0.0f ? x.x : 0.0f;
+      x.y = x.y > 0.0f ? x.y : 0.0f;
+      x.z = x.z > 0.0f ? x.z : 0.0f;
+      x.w = x.w > 0.0f ? x.w : 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < NACC; ++t) {
+      const float b0 = cv[t] ? wc[t][(int64_t)k * ldw] : 0.0f, b1 = cv[t] ? wc[t][(int64_t)(k + 2) * ldw] : 0.0f;
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? x.y : x.x, b0, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? x.w : x.z, b1, acc[t], 0, 0, 0);
+    }
+  }
+  // one accumulator at a time through LDS; wave w finishes registers r = w, w + SLICES, ... of it
+  // (slice sums in slice order)
+#pragma unroll
+  for (int t = 0; t < NACC; ++t) {
+    if (t) __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) part[w][r][lane] = acc[t][r];
+    __syncthreads();
+    const int c = col0 + 32 * t + i;
+    for (int r = w; r < 16; r += SLICES) {
+      float v = part[0][r][lane];
+      for (int q = 1; q < SLICES; ++q) v = v + part[q][r][lane];
+      const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (row >= M || c >= N) continue;
+      if (b) v = v + b[c];
+      if (flags & F_RELU_OUT) v = v > 0.0f ? v : 0.0f;
+      if (flags & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
+      float* y = Y + (int64_t)row * ldy + c;
+      *y = (flags & F_ACCUM) ? *y + v : v;
+    }
   }
 }
 
@@ -792,21 +875,8 @@ struct pst_decoder {
   float* d_pe_tok = nullptr;   // PE(t; 512/df) [512/df][128]
   float* d_pe_rel = nullptr;   // PE(d; 512), d = -511..511 [1023][128]
   float* d_pw = nullptr;       // IPA point weights [12]
-  rocblas_handle blas = nullptr;  // library GEMMs (per-node rows; pair rows only when unfused)
-  // hipBLASLt GEMMs with the bias / ReLU epilogue fused (see gemm_any); plans cached per shape
-  struct LtPlan {
-    hipblasLtMatmulDesc_t desc = nullptr;
-    hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
-    hipblasLtMatmulAlgo_t algo{};
-    size_t ws = 0;
-    bool ok = false;
-  };
   float* d_ipa_w = nullptr;  // [384][1152]: q_scalar | kv_scalar | q_point | kv_point weights
   float* d_ipa_b = nullptr;  // [1152] their biases
-  hipblasLtHandle_t lt = nullptr;
-  void* lt_ws = nullptr;
-  size_t lt_ws_bytes = 0;
-  std::map<std::array<int64_t, 7>, LtPlan> lt_plans;
   DecWeights W{};
   float* d_pair = nullptr;  // fused pair kernel: fragments, perm vectors, U table (k_pair_fused)
   PairArgs pair{};          // pointers into d_pair (per-call fields filled by decode_group)
@@ -914,11 +984,10 @@ size_t walk_decoder(const float* base, int D, DecWeights* W) {
   return o;
 }
 
-// GEMMs go to rocBLAS (row-major Y = X·W as column-major Yᵀ = Wᵀ·Xᵀ; accumulation via β = 1) with
-// a bias/activation epilogue; an input ReLU is applied into a scratch copy first. k_gemm is the
-// self-contained fallback (PST_DECODE_NO_BLAS=1). Set by decode_one for the current context.
-thread_local rocblas_handle t_blas = nullptr;
-thread_local float* t_relu_buf = nullptr;  // [512 × 2112] scratch for F_RELU_IN operands
+// Every decode GEMM is in-tree: k_gemm_mfma (f32 MFMA), or the LDS-tiled VALU k_gemm when the
+// operands do not meet its alignment (or PST_DECODE_NO_MFMA=1, for the A/B test). Both compute
+// the same fma chains.
+thread_local bool t_mfma = true;  // set by decode_group for the current call
 
 __global__ __launch_bounds__(256) void k_relu_copy(const float* __restrict__ X, int ldx, float* __restrict__ Y,
                                                    int64_t M, int K) {
@@ -930,70 +999,25 @@ __global__ __launch_bounds__(256) void k_relu_copy(const float* __restrict__ X, 
   }
 }
 
-thread_local pst_decoder* t_lt = nullptr;  // decoder whose hipBLASLt state gemm_any uses
-
-// plan (descriptor, layouts, heuristic algorithm) for D[N×M] = act(Wᵀ·Xᵀ + β·C + b), column-major
-pst_decoder::LtPlan* lt_plan(pst_decoder* d, int M, int N, int K, int ldx, int ldy, hipblasLtEpilogue_t ep,
-                             bool accum) {
-  const std::array<int64_t, 7> key{M, N, K, ldx, ldy, (int64_t)ep, accum ? 1 : 0};
-  auto it = d->lt_plans.find(key);
-  if (it != d->lt_plans.end()) return it->second.ok ? &it->second : nullptr;
-  pst_decoder::LtPlan& p = d->lt_plans[key];
-  if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return nullptr;
-  const uint32_t epv = (uint32_t)ep;
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epv, sizeof(epv));
-  if (ep == HIPBLASLT_EPILOGUE_BIAS || ep == HIPBLASLT_EPILOGUE_RELU_BIAS) {
-    const hipDataType bt = HIP_R_32F;
-    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
-  }
-  if (hipblasLtMatrixLayoutCreate(&p.a, HIP_R_32F, N, K, N) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.b, HIP_R_32F, K, M, ldx) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.c, HIP_R_32F, N, M, ldy) != HIPBLAS_STATUS_SUCCESS)
-    return nullptr;
-  hipblasLtMatmulPreference_t pref = nullptr;
-  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return nullptr;
-  const uint64_t wsb = d->lt_ws_bytes;
-  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
-  hipblasLtMatmulHeuristicResult_t res[1];
-  int n = 0;
-  const hipblasStatus_t hs =
-      hipblasLtMatmulAlgoGetHeuristic(d->lt, p.desc, p.a, p.b, p.c, p.c, pref, 1, res, &n);
-  hipblasLtMatmulPreferenceDestroy(pref);
-  if (hs != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].workspaceSize > d->lt_ws_bytes) return nullptr;
-  p.algo = res[0].algo;
-  p.ws = res[0].workspaceSize;
-  p.ok = true;
-  return &p;
-}
-
 inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, int K, int N, const float* b, float* Y,
                      int ldy, int M, int flags) {
-  if (t_blas && (!(flags & F_RELU_IN) || (int64_t)M * K <= 512 * 2112)) {
-    if (flags & F_RELU_IN) {
-      hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, X, ldx, t_relu_buf, (int64_t)M, K);
-      X = t_relu_buf;
-      ldx = K;
-    }
-    const float one = 1.0f, beta = (flags & F_ACCUM) ? 1.0f : 0.0f;
-    // hipBLASLt with the bias / ReLU fused into the GEMM epilogue: act(X·W + β·Y + b), the same
-    // expression the rocBLAS + k_bias_act pair below evaluates in two launches
-    if (t_lt && !(flags & F_SIGMOID_OUT)) {
-      const bool relu = flags & F_RELU_OUT;
-      const hipblasLtEpilogue_t ep = b ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS)
-                                       : (relu ? HIPBLASLT_EPILOGUE_RELU : HIPBLASLT_EPILOGUE_DEFAULT);
-      pst_decoder::LtPlan* p = lt_plan(t_lt, M, N, K, ldx, ldy, ep, flags & F_ACCUM);
-      if (p) {
-        if (b) hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &b, sizeof(b));
-        if (hipblasLtMatmul(t_lt->lt, p->desc, &one, Wt, p->a, X, p->b, &beta, Y, p->c, Y, p->c, &p->algo,
-                            t_lt->lt_ws, p->ws, st) == HIPBLAS_STATUS_SUCCESS)
-          return;
-      }
-    }
-    rocblas_sgemm(t_blas, rocblas_operation_none, rocblas_operation_none, N, M, K, &one, Wt, N, X, ldx, &beta, Y, ldy);
-    if (b || (flags & (F_RELU_OUT | F_SIGMOID_OUT))) {
-      hipLaunchKernelGGL(k_bias_act, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, Y, ldy, b, (int64_t)M, N,
-                         flags & (F_RELU_OUT | F_SIGMOID_OUT));
-    }
+  if (M <= 0) return;
+  if (t_mfma && K % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0) {
+    // one 32-column accumulator per wave and K split into slices of <= ~130: the operand loads
+    // per MFMA are the same for any split, while more slices mean more waves in flight and
+    // shorter dependent chains (measured on 8 x 256 decodes: four accumulators per wave with 4/16
+    // slices 7.05 ms, one with 4/8 slices 6.08 ms)
+    auto go = [&](auto kern, int slices) {
+      const int ks = (K / slices + 3) / 4 * 4;
+      dim3 grid((unsigned)((N + 31) / 32), (unsigned)((M + 31) / 32));
+      hipLaunchKernelGGL(kern, grid, dim3(64 * slices), 0, st, X, ldx, Wt, N, b, Y, ldy, M, N, K, flags, ks);
+    };
+    if (K >= 1024)
+      go(k_gemm_mfma<16, 1>, 16);
+    else if (K >= 256)
+      go(k_gemm_mfma<8, 1>, 8);
+    else
+      go(k_gemm_mfma<4, 1>, 4);
     return;
   }
   dim3 grid((N + 63) / 64, (M + 63) / 64);
@@ -1022,7 +1046,7 @@ struct Scratch {
   float *orig_in, *orig, *res, *ln_a, *ln_b, *q, *k, *v, *gate, *wavg, *tr_h;
   float *left, *right, *P, *h1, *pair0, *catb, *lin_out, *lnz, *z, *zln, *b2d;
   float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
-  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *relu_buf, *kT, *kpT, *init_relu, *ipa_in;
+  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *kT, *kpT, *init_relu, *ipa_in;
   int64_t *tok_off, *node_off, *pair_off;
   int32_t *tok_prot, *node_prot;
   uint32_t* tokens;
@@ -1052,7 +1076,7 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
                 {(void**)&S->scb, NN * 128 * F},     {(void**)&S->sct, NN * 128 * F},  {(void**)&S->unnorm, NN * 6 * F},
                 {(void**)&S->angles, 8 * NN * 6 * F}, {(void**)&S->traj, 8 * NN * 7 * F},
                 {(void**)&S->atom37, NN * 111 * F},  {(void**)&S->atom14, NN * 42 * F},
-                {(void**)&S->relu_buf, NN * 2112 * F}, {(void**)&S->kT, NN * 192 * F}, {(void**)&S->kpT, NN * 144 * F},
+                {(void**)&S->kT, NN * 192 * F}, {(void**)&S->kpT, NN * 144 * F},
                 {(void**)&S->init_relu, NN * 128 * F},
                 {(void**)&S->tok_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->node_off, (NN + 1) * sizeof(int64_t)},
                 {(void**)&S->pair_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->tok_prot, NN * sizeof(int32_t)},
@@ -1090,9 +1114,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   const DecWeights& W = dec->W;
   hipStream_t st = dec->stream;
   const int64_t T = G.T, N = G.N, NP = G.NP;
-  t_blas = getenv("PST_DECODE_NO_BLAS") ? nullptr : dec->blas;
-  t_lt = (t_blas && dec->lt && !getenv("PST_DECODE_NO_LT")) ? dec : nullptr;
-  t_relu_buf = S.relu_buf;
+  t_mfma = !getenv("PST_DECODE_NO_MFMA");
   DCHK(hipMemcpyAsync(S.tokens, G.tokens.data(), sizeof(uint32_t) * T, hipMemcpyHostToDevice, st));
   DCHK(hipMemcpyAsync(S.tok_off, G.tok_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
   DCHK(hipMemcpyAsync(S.node_off, G.node_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
@@ -1350,17 +1372,6 @@ int pst_decoder_create(int32_t device, const pst_model_desc* desc, const float* 
   };
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&dec->stream, hipStreamNonBlocking) != hipSuccess)
     return bad("hip stream creation failed");
-  if (rocblas_create_handle(&dec->blas) != rocblas_status_success ||
-      rocblas_set_stream(dec->blas, dec->stream) != rocblas_status_success)
-    return bad("rocblas handle creation failed");
-  // hipBLASLt is optional: without it (or a plan for a shape) the rocBLAS path runs
-  dec->lt_ws_bytes = (size_t)32 << 20;
-  if (hipblasLtCreate(&dec->lt) != HIPBLAS_STATUS_SUCCESS || hipMalloc(&dec->lt_ws, dec->lt_ws_bytes) != hipSuccess) {
-    if (dec->lt) (void)hipblasLtDestroy(dec->lt);
-    dec->lt = nullptr;
-    dec->lt_ws = nullptr;
-    dec->lt_ws_bytes = 0;
-  }
   if (hipMalloc(&dec->d_blob, n_params * sizeof(float)) != hipSuccess ||
       hipMemcpy(dec->d_blob, params, n_params * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
     return bad("decoder weight upload failed");
@@ -1418,14 +1429,6 @@ int pst_decoder_destroy(pst_decoder* dec) {
                   (void*)dec->d_pe_rel, (void*)dec->d_pw, (void*)dec->d_pair, dec->ws, (void*)dec->d_ipa_w,
                   (void*)dec->d_ipa_b})
     if (p) (void)hipFree(p);
-  if (dec->blas) (void)rocblas_destroy_handle(dec->blas);
-  for (auto& kv : dec->lt_plans) {
-    if (kv.second.desc) (void)hipblasLtMatmulDescDestroy(kv.second.desc);
-    for (hipblasLtMatrixLayout_t l : {kv.second.a, kv.second.b, kv.second.c})
-      if (l) (void)hipblasLtMatrixLayoutDestroy(l);
-  }
-  if (dec->lt_ws) (void)hipFree(dec->lt_ws);
-  if (dec->lt) (void)hipblasLtDestroy(dec->lt);
   if (dec->stream) (void)hipStreamDestroy(dec->stream);
   delete dec;
   return PST_OK;

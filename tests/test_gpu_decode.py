@@ -57,6 +57,45 @@ def test_decode_matches_reference(case, monkeypatch):
     assert np.all(atoms[~mask] == 0)
 
 
+WIDE = os.path.join(os.path.dirname(__file__), "golden", "decode_ref_wide.npz")
+
+
+def _wide_cases():
+    if not os.path.exists(WIDE):
+        return []
+    F = np.load(WIDE)
+    return sorted({k.split("/")[0] for k in F.files})
+
+
+@pytest.mark.parametrize("case", _wide_cases())
+def test_decode_matches_reference_wide(case, monkeypatch):
+    """128-512 tokens at df 1 / 2 / 4 (decode_ref_wide.npz, make_decode_golden.py wide): the same
+    quantities and tolerances as above; the pair representation is stored for 4 rows i (all j)."""
+    monkeypatch.setenv("PST_DEBUG", "1")
+    from pst_amd._native import Decoder
+    F = np.load(WIDE)
+    cb, df, T, N, D, pseed = (int(v) for v in F[case + "/meta"])
+    blob = P.pack_decoder(P.random_full_params(D, pseed), D)
+    dec = Decoder(0, cb, df, blob)
+    atoms = dec.decode([F[case + "/tokens"]])[0]
+    single = dec.debug(0, N * 128).reshape(N, 128)
+    pair = dec.debug(1, N * N * 128).reshape(N, N, 128)[F[case + "/pair_rows"]]
+    traj = dec.debug(2, 8 * N * 7).reshape(8, N, 7)
+    dec.close()
+    err = lambda a, b: float(np.max(np.abs(a - b)))
+    e_single = err(single, F[case + "/single"])
+    e_pair = err(pair, F[case + "/pair"]) / float(np.max(np.abs(F[case + "/pair"])))
+    e_traj = err(traj, F[case + "/traj"])
+    e_atoms = err(atoms, F[case + "/atom37"])
+    print(f"{case}: single {e_single:.2e} pair(rel) {e_pair:.2e} traj {e_traj:.2e} atoms {e_atoms:.2e}")
+    assert atoms.shape == (N, 37, 3)
+    assert e_single < TOL_SINGLE
+    assert e_pair < TOL_PAIR_REL
+    assert e_traj < TOL_TRAJ
+    assert e_atoms < TOL_ATOMS
+    assert np.all(atoms[~F[case + "/atom37_mask"].astype(bool)] == 0)
+
+
 def test_decode_cli_end_to_end(tmp_path):
     """tokens → `decode_tokens.py` → structures/structure_<stem>.pdb, coordinates equal to the
     decoder's (PDB %8.3f rounding) and 4 backbone atoms per residue."""
@@ -143,20 +182,20 @@ def test_fused_pair_kernel_matches_library_path(monkeypatch):
         assert np.max(np.abs(a - b)) < 1e-3
 
 
-def test_gemm_backends_agree(monkeypatch):
-    """The per-node GEMMs on hipBLASLt with the fused bias/ReLU epilogue (default), on rocBLAS +
-    the epilogue kernel (PST_DECODE_NO_LT=1) and on the in-tree LDS-tiled kernel
-    (PST_DECODE_NO_BLAS=1) give the same structures to float32 reordering noise."""
+def test_gemm_mfma_matches_valu_gemm(monkeypatch):
+    """The per-node GEMMs run on the in-tree split-K f32-MFMA kernel (k_gemm_mfma, default) or on
+    the LDS-tiled VALU kernel (PST_DECODE_NO_MFMA=1, one fma chain over k). The split K changes
+    only the f32 summation order: whole decodes agree to float32 reordering noise (ragged group of
+    three proteins, odd sizes: row and column tails of the tiles)."""
     from pst_amd._native import Decoder
     rng = np.random.default_rng(17)
     toks = [rng.integers(0, 4096, n) for n in (64, 23, 130)]
     dec = Decoder(0, 4096, 1, P.pack_decoder(P.random_full_params(6, 13), 6))
     base = dec.decode(toks)
-    for env in ("PST_DECODE_NO_LT", "PST_DECODE_NO_BLAS"):
-        monkeypatch.setenv(env, "1")
-        other = dec.decode(toks)
-        monkeypatch.delenv(env)
-        for a, b in zip(base, other):
-            assert np.all(np.isfinite(b))
-            assert np.max(np.abs(a - b)) < 1e-3, env
+    monkeypatch.setenv("PST_DECODE_NO_MFMA", "1")
+    other = dec.decode(toks)
+    monkeypatch.delenv("PST_DECODE_NO_MFMA")
     dec.close()
+    for a, b in zip(base, other):
+        assert np.all(np.isfinite(a)) and np.all(np.isfinite(b))
+        assert np.max(np.abs(a - b)) < 1e-3
