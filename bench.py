@@ -120,6 +120,21 @@ def spawn_workers(n: int) -> int:
     return rc
 
 
+def init_group(backend: str, **kw) -> None:
+    """dist.init_process_group with the gloo transport's connection banner (printed on the
+    process's stdout) sent to stderr: stdout carries only the JSON line."""
+    import torch.distributed as dist
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group(backend, **kw)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def shard_ids(args, rank, world):
     """Protein ids of this rank (protein p is synthetic_protein(residues, seed 1000 + p))."""
     from pst_amd import runner
@@ -140,7 +155,7 @@ def plan_only(args, rank, world):
     import torch
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("gloo")
+        init_group("gloo")
     ids = shard_ids(args, rank, world)
     t = torch.tensor([len(ids), len(ids) * args.residues], dtype=torch.int64)
     allids = [None] * world
@@ -297,9 +312,9 @@ def main():
     if world > 1:
         torch.cuda.set_device(gpu)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            init_group("nccl", device_id=torch.device("cuda", gpu))
         else:
-            dist.init_process_group(args.dist_backend)
+            init_group(args.dist_backend)
     dev = torch.device("cuda", gpu)
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     seen_world = dist.get_world_size() if world > 1 else 1
