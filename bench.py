@@ -237,8 +237,7 @@ def casp14_end_to_end(tk):
             tok, nt, _ = tk.tokenize_packed(B.positions, B.flags, B.offsets)
             t2 = time.perf_counter()
             save_npy_files([os.path.join(out, os.path.basename(f)[:-4] + "_tokens") for f in files],
-                           [tok[int(B.offsets[i]):int(B.offsets[i]) + nt[i]].reshape(1, -1) for i in range(len(files))],
-                           threads=threads)
+                           [tok[int(B.offsets[i]):int(B.offsets[i]) + nt[i]].reshape(1, -1) for i in range(len(files))])
             t3 = time.perf_counter()
             R = int(B.offsets[-1])
             res = {"workload": "CASP14 31 structures (SURVEY config 2), codebook 4096, df 1", "residues": R,

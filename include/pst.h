@@ -220,6 +220,13 @@ int pst_pdb_batch_copy(const pst_pdb_batch* b, double* positions, uint8_t* flags
 const char* pst_pdb_batch_error(const pst_pdb_batch* b, int32_t i);
 void pst_pdb_batch_free(pst_pdb_batch* b);
 
+/* Token-file output of the tokenize loop (scripts/inference_runner.py:313-321 writes one
+ * np.save per protein): n whole files written (created / truncated) from host buffers on
+ * n_threads threads of libpst's host pool; the caller builds the .npy bytes. PST_E_INVALID if
+ * any file could not be written. */
+int pst_write_files(int32_t n, const char* const* paths, const void* const* data, const size_t* lens,
+                    int32_t n_threads);
+
 /* Per-stage timing of the last tokenize call (HIP events on the context's stream):
  * ms[0..5] = prep, knn, mpnn layer 0, mpnn layer 1, mpnn layer 2, downsampler+FSQ. */
 #define PST_N_STAGES 6

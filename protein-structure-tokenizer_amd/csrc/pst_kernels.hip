@@ -517,15 +517,26 @@ __device__ __forceinline__ void agg_from_gsum(Tile& ag, const float* __restrict_
 
 // acc += x[features] · Wf over the 32 (27 + zero pad) edge features, 16 MFMA k-steps;
 // x[r] holds features (r&3) + 8(r>>2) + 4·half (the k order of the fragments)
+// (fragments through a buffer resource with constant SGPR offsets and a FEAT_DEPTH-deep register
+// ring, as tile_gemm_f: no per-k-step 64-bit addresses; k_mpnn<0> 8.60 -> 8.45 ms)
+#ifndef FEAT_DEPTH
+#define FEAT_DEPTH 4
+#endif
 __device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const float4* __restrict__ Wf) {
-  const float4* wf = Wf + lane_id();
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
+  const int vo = lane_id() * 16;
+  float4 ring[FEAT_DEPTH];
+#pragma unroll
+  for (int i = 0; i < FEAT_DEPTH; ++i) ring[i] = buf_load4(rs, vo, i * 1024);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    float4 wa = wf[r * 64];
+    const float4 wa = ring[r % FEAT_DEPTH];
+    if (r + FEAT_DEPTH < 16) ring[r % FEAT_DEPTH] = buf_load4(rs, vo, (r + FEAT_DEPTH) * 1024);
     acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, x[r], acc.m[0], 0, 0, 0);
     acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, x[r], acc.m[1], 0, 0, 0);
     acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, x[r], acc.m[2], 0, 0, 0);
     acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, x[r], acc.m[3], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 

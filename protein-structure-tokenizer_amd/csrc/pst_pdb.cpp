@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/pst.h"
+#include "pst_pool.h"
 #include "pst_residue_tables.h"
 
 namespace {
@@ -453,9 +454,9 @@ struct pst_pdb_batch {
 
 namespace {
 
-// fn(i) for i < n on n_threads threads, largest `size` first (the biggest file bounds the call)
+// fn(i) for i < n on n_threads threads of the process-wide pool, largest `size` first (the biggest
+// file bounds the call)
 int run_pool(int32_t n, int32_t n_threads, const std::function<size_t(int)>& size, const std::function<void(int)>& fn) {
-  int T = std::max(1, std::min<int>(n_threads > 0 ? n_threads : 1, n));
   std::vector<int> order(n);
   std::vector<size_t> sz(n);
   for (int i = 0; i < n; ++i) {
@@ -463,14 +464,7 @@ int run_pool(int32_t n, int32_t n_threads, const std::function<size_t(int)>& siz
     sz[i] = size(i);
   }
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return sz[a] > sz[b]; });
-  std::atomic<int> next(0);
-  auto worker = [&]() {
-    for (int i = next++; i < n; i = next++) fn(order[i]);
-  };
-  std::vector<std::thread> th;
-  for (int t = 1; t < T; ++t) th.emplace_back(worker);
-  worker();
-  for (auto& t : th) t.join();
+  pst::HostPool::get().run(n, n_threads > 0 ? n_threads : 1, [&](int i) { fn(order[i]); });
   return PST_OK;
 }
 
@@ -580,5 +574,19 @@ const char* pst_pdb_batch_error(const pst_pdb_batch* b, int32_t i) {
 }
 
 void pst_pdb_batch_free(pst_pdb_batch* b) { delete b; }
+
+int pst_write_files(int32_t n, const char* const* paths, const void* const* data, const size_t* lens,
+                    int32_t n_threads) {
+  if (n < 0 || (n > 0 && (!paths || !data || !lens))) return PST_E_INVALID;
+  std::atomic<int> failed(-1);
+  pst::HostPool::get().run(n, n_threads > 0 ? n_threads : 1, [&](int i) {
+    FILE* f = fopen(paths[i], "wb");
+    bool ok = f != nullptr;
+    if (ok && lens[i]) ok = fwrite(data[i], 1, lens[i], f) == lens[i];
+    if (f && fclose(f) != 0) ok = false;
+    if (!ok) failed.store(i);
+  });
+  return failed.load() < 0 ? PST_OK : PST_E_INVALID;
+}
 
 }  // extern "C"

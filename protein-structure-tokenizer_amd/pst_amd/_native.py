@@ -37,7 +37,7 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_tokenize", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
            "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing", "pst_device_count",
            "pst_codebook_aux_device", "pst_pdb_parse_files", "pst_pdb_parse_strings",
-           "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free",
+           "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free", "pst_write_files",
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
            "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_debug", "pst_build_graph")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
@@ -93,6 +93,7 @@ def lib():
         L.pst_pdb_batch_error.restype = ctypes.c_char_p
         L.pst_pdb_batch_error.argtypes = [P, ctypes.c_int32]
         L.pst_pdb_batch_free.argtypes = [P]
+        L.pst_write_files.argtypes = [ctypes.c_int32, P, P, P, ctypes.c_int32]
         L.pst_decoder_param_count.restype = ctypes.c_size_t
         L.pst_decoder_param_count.argtypes = [ctypes.c_int32]
         L.pst_decoder_create.argtypes = [ctypes.c_int32, ctypes.POINTER(_ModelDesc), P, ctypes.c_size_t, ctypes.POINTER(P)]
@@ -191,6 +192,20 @@ def parse_pdb_strings(texts: Sequence[str], chain_id: Optional[str] = None, n_th
     if rc != PST_OK:
         raise PstError(f"pst_pdb_parse_strings failed: {rc}")
     return _collect_pdb(h)
+
+
+def write_files(paths: Sequence[str], blobs: Sequence[bytes], n_threads: int = 8) -> None:
+    """Write whole files from byte strings on libpst's host thread pool (pst_write_files)."""
+    n = len(paths)
+    if n == 0:
+        return
+    enc = [os.fsencode(p) for p in paths]
+    parr = (ctypes.c_char_p * n)(*enc)
+    darr = (ctypes.c_char_p * n)(*blobs)
+    larr = (ctypes.c_size_t * n)(*[len(b) for b in blobs])
+    rc = lib().pst_write_files(n, parr, darr, larr, n_threads)
+    if rc != PST_OK:
+        raise OSError(f"pst_write_files failed for one of {n} files (first: {paths[0]})")
 
 
 def pack_samples(samples) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

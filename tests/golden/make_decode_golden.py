@@ -7,7 +7,10 @@ keep the intermediates) with `random_full_params` weights, at the reference's ow
 representation (s_i), pair representation z_ij, the 8 per-layer affines (traj), backbone
 torsion sin/cos, atom14 positions and final atom37 positions. ~10 minutes per case.
 
-    python tests/golden/make_decode_golden.py
+    python tests/golden/make_decode_golden.py          # decode_golden_f64.npz (2 small cases)
+    python tests/golden/make_decode_golden.py wide     # decode_ref_wide.npz (128-512 tokens)
+
+The wide cases keep the pair representation only for PAIR_ROWS rows i (all j) to stay small.
 """
 import os
 import sys
@@ -18,9 +21,13 @@ sys.path.insert(0, HERE)
 
 # (name, codebook, df, n_tokens, token seed, param seed)
 CASES = [("dec_k4096_df1_t40", 4096, 1, 40, 1, 77), ("dec_k64000_df4_t14", 64000, 4, 14, 2, 78)]
+# 128-512 tokens, df 1 / 2 / 4, two level sets (decode depth)
+CASES_WIDE = [("dec_k4096_df1_t128", 4096, 1, 128, 11, 81), ("dec_k4096_df1_t512", 4096, 1, 512, 12, 82),
+              ("dec_k64000_df4_t128", 64000, 4, 128, 13, 83), ("dec_k4096_df2_t256", 4096, 2, 256, 14, 84)]
+PAIR_ROWS = 4
 
 
-def main():
+def main(wide=False):
     import _refenv
     _refenv.activate(f64=True)
     import numpy as np
@@ -30,7 +37,13 @@ def main():
     from pst_amd.config import LEVELS, load_config, overrides_for
 
     out = {}
-    for name, cb, df, T, tseed, pseed in CASES:
+    wide_path = os.path.join(HERE, "decode_ref_wide.npz")
+    if wide and os.path.exists(wide_path):  # resume: keep the cases already made
+        with np.load(wide_path) as old:
+            out = {k: old[k] for k in old.files}
+    for name, cb, df, T, tseed, pseed in (CASES_WIDE if wide else CASES):
+        if name + "/meta" in out:
+            continue
         t0 = time.time()
         cfg = load_config("vq3d_inference", overrides=overrides_for(cb, df),
                           config_path=os.path.join(_refenv.REF, "config", "structure_tokenizer"))
@@ -63,7 +76,12 @@ def main():
         out[pre + "codes"] = np.asarray(codes)[0, :T].astype(np.float32)
         out[pre + "up_proj"] = np.asarray(qp)[0, :T].astype(np.float32)
         out[pre + "single"] = np.asarray(s_i)[0, :N].astype(np.float32)
-        out[pre + "pair"] = np.asarray(z)[0, :N, :N].astype(np.float32)
+        if wide:  # rows 0, N/3, 2N/3, N-1 of z_ij (all j)
+            rows = np.unique(np.linspace(0, N - 1, PAIR_ROWS).astype(np.int64))
+            out[pre + "pair_rows"] = rows
+            out[pre + "pair"] = np.asarray(z)[0, rows, :N].astype(np.float32)
+        else:
+            out[pre + "pair"] = np.asarray(z)[0, :N, :N].astype(np.float32)
         out[pre + "traj"] = np.asarray(st["traj"])[0, :, :N].astype(np.float32)
         out[pre + "angles"] = np.asarray(st["sidechains"]["angles_sin_cos"])[0, :, :N].astype(np.float32)
         ap = st["sidechains"]["atom_pos"]
@@ -71,8 +89,11 @@ def main():
         out[pre + "atom37"] = np.asarray(st["final_atom_positions"])[0, :N].astype(np.float32)
         out[pre + "atom37_mask"] = np.asarray(st["final_atom_mask"])[0, :N].astype(np.uint8)
         print(name, "done in", round(time.time() - t0), "s", flush=True)
-    np.savez_compressed(os.path.join(HERE, "decode_golden_f64.npz"), **out)
+        if wide:  # checkpoint after every case (each takes minutes)
+            np.savez_compressed(wide_path, **out)
+    if not wide:
+        np.savez_compressed(os.path.join(HERE, "decode_golden_f64.npz"), **out)
 
 
 if __name__ == "__main__":
-    main()
+    main(wide=len(sys.argv) > 1 and sys.argv[1] == "wide")
