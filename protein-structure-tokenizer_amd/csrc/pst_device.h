@@ -517,19 +517,34 @@ __device__ __forceinline__ float tile_split_sum(const Tile& t) {
 
 // LayerNorm / MaskedLayerNorm (mask 1) over the 128 channels of each column, in place.
 // scale/offset are perm-ordered 128-vectors.
+// The elementwise steps run as pinned packed pairs (v_pk_add/mul_f32, as the GELU): d = x - mean
+// is formed once and kept in place of x (the normalisation used to recompute it), d·d pairwise;
+// only the variance sum stays a scalar chain (its order is canonical). Same operations, same
+// bits as the scalar form: x - m == x + (-m) in IEEE arithmetic, products and sums unchanged.
+__device__ __forceinline__ f32x2 apk_add(f32x2 a, f32x2 b) {
+  f32x2 d;
+  asm("v_pk_add_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
 __device__ __forceinline__ void tile_layer_norm(Tile& t, const float* __restrict__ scale,
                                                 const float* __restrict__ offset) {
   float mean = tile_split_sum(t) / 128.0f;
+  const f32x2 nm = {-mean, -mean};
   float s = 0.0f;
 #pragma unroll
   for (int M = 0; M < 4; ++M)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float d = t.m[M][r] - mean;
-      s = s + d * d;
+    for (int r = 0; r < 16; r += 2) {
+      const f32x2 d = apk_add((f32x2){t.m[M][r], t.m[M][r + 1]}, nm);
+      const f32x2 dd = apk_mul(d, d);
+      s = s + dd.x;
+      s = s + dd.y;
+      t.m[M][r] = d.x;
+      t.m[M][r + 1] = d.y;
     }
   float var = (s + partner(s)) / 128.0f;
   float rs = 1.0f / sqrtf(var + 1e-5f);
+  const f32x2 rr = {rs, rs};
   const float4* ps = reinterpret_cast<const float4*>(scale + (lane_id() >> 5) * 64);
   const float4* po = reinterpret_cast<const float4*>(offset + (lane_id() >> 5) * 64);
 #pragma unroll
@@ -538,12 +553,13 @@ __device__ __forceinline__ void tile_layer_norm(Tile& t, const float* __restrict
     for (int q = 0; q < 4; ++q) {
       __builtin_amdgcn_sched_barrier(0);
       float4 sc = ps[M * 4 + q], of = po[M * 4 + q];
-      float scv[4] = {sc.x, sc.y, sc.z, sc.w}, ofv[4] = {of.x, of.y, of.z, of.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float inv = scv[i] * rs;
-        t.m[M][4 * q + i] = inv * (t.m[M][4 * q + i] - mean) + ofv[i];
-      }
+      const f32x2 inv0 = apk_mul((f32x2){sc.x, sc.y}, rr), inv1 = apk_mul((f32x2){sc.z, sc.w}, rr);
+      const f32x2 y0 = apk_add(apk_mul(inv0, (f32x2){t.m[M][4 * q], t.m[M][4 * q + 1]}), (f32x2){of.x, of.y});
+      const f32x2 y1 = apk_add(apk_mul(inv1, (f32x2){t.m[M][4 * q + 2], t.m[M][4 * q + 3]}), (f32x2){of.z, of.w});
+      t.m[M][4 * q] = y0.x;
+      t.m[M][4 * q + 1] = y0.y;
+      t.m[M][4 * q + 2] = y1.x;
+      t.m[M][4 * q + 3] = y1.y;
     }
 }
 
