@@ -573,13 +573,16 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
   float x[16];  // layer 0: this lane's edge features
   int lr0 = 0, ls0 = 0;
   if (LAYER == 0) {
-    // init_edge_embed: chain from T[s-r] (= b + edgePE(s-r) W[0:128]) over the 27 (+5 zero) features
-    int lr = a.node_local[g], ls = a.node_local[s];
+    // init_edge_embed: chain from T[s-r] (= b + edgePE(s-r) W[0:128]) over the 27 (+5 zero) features.
+    // A protein's nodes sit in consecutive slots (slot = protein base + local index, k_prep), so
+    // ls - lr = s - g without reading node_local[s]; gap/padding receivers have self edges
+    // (s = g) and lr clamped to 0, hence ls = 0 as before. The T row then needs no load at all.
+    const int d = (int)(s - g);
+    int lr = a.node_local[g];
     lr = lr < 0 ? 0 : lr;
-    ls = ls < 0 ? lr : ls;
     lr0 = lr;
-    ls0 = ls;
-    tile_load_perm(e, a.Ttab + (int64_t)(ls - lr + 511) * 128);
+    ls0 = lr + d;
+    tile_load_perm(e, a.Ttab + (int64_t)(d + 511) * 128);
     const float4* fp = reinterpret_cast<const float4*>(a.feat + E * 32 + 4 * (lane >> 5));
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
