@@ -28,9 +28,15 @@ constexpr int KNN = 50;
 // through HBM). Split wins below ~1 000 tasks and in the half-empty rounds above.
 constexpr double SPLIT_COST_PER_TASK = 1.05;  // one edge block per wave (re-measured, tools/policy_check.sh)
 constexpr double FUSED_SINGLE_ROUND = 1.1;
+// A single round more than half full runs the fused layers with two waves per task
+// (use_half_tasks): both wave slots of every SIMD busy, about one round of full-size cost plus
+// the node update on one wave.
+constexpr double FUSED_HALF_ROUND = 1.02;
+bool use_half_tasks(int64_t n_tasks, int64_t n_simds) { return 2 * n_tasks > n_simds && n_tasks <= n_simds; }
 bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
   const int64_t k = (n_tasks + n_simds - 1) / n_simds;
-  const double fused = k <= 1 ? FUSED_SINGLE_ROUND * (double)n_simds : (double)(k * n_simds);
+  const double single = use_half_tasks(n_tasks, n_simds) ? FUSED_HALF_ROUND : FUSED_SINGLE_ROUND;
+  const double fused = k <= 1 ? single * (double)n_simds : (double)(k * n_simds);
   return SPLIT_COST_PER_TASK * (double)n_tasks < fused;
 }
 
@@ -221,6 +227,7 @@ struct pst_ctx {
   int64_t edge_waves = -2;   // PST_EDGE_WAVES: split-schedule edge waves target; -1 = SPLIT_EDGE_WAVES
   int64_t node_coop = -2;    // PST_NODE_COOP: k_mpnn_node_coop iff split and n_tasks <= this; -1 = default
   int64_t down_coop = -2;    // PST_DOWN_COOP: k_down_coop iff n_tiles <= this; -1 = default; -2 = not read yet
+  int64_t half_tasks = -2;   // PST_HALF_TASKS: 1 = fused layers always two waves per task, 0 = never; -1 = policy
   std::vector<int64_t> h_offsets;
   // pst_tokenize's H2D pipeline: proteins copied in chunks on copy_stream, chunk k+1's copy
   // overlapping chunk k's compute on `stream` (H2D_MAX_CHUNKS events)
@@ -549,6 +556,8 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   env_threshold(ctx->node_coop, "PST_NODE_COOP");
   const bool node_coop =
       split && n_tasks <= (ctx->node_coop >= 0 ? ctx->node_coop : (int64_t)(NODE_COOP_SIMD_FRACTION * ctx->n_simds));
+  env_threshold(ctx->half_tasks, "PST_HALF_TASKS");
+  const bool half = !split && (ctx->half_tasks >= 0 ? ctx->half_tasks != 0 : use_half_tasks(n_tasks, ctx->n_simds));
   float* msg_rows = nullptr;
   int32_t bpw = 1;
   if (split) {
@@ -577,6 +586,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.n_tasks = n_tasks;
     m.msg_rows = msg_rows;
     m.blocks_per_wave = bpw;
+    m.half_tasks = half ? 1 : 0;
     m.senders = w.senders;
     m.deg = w.deg;
     m.node_local = w.node_local;

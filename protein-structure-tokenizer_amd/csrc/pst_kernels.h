@@ -81,6 +81,7 @@ struct MpnnArgs {
   // split mode (k_mpnn_edge + k_mpnn_node) when non-null: per-edge messages [E][128] (perm rows)
   float* msg_rows;
   int32_t blocks_per_wave;  // edge blocks of 32 per k_mpnn_edge wave
+  int32_t half_tasks;       // fused mode: two waves per task (k_mpnn<L, true>; n_tasks % 4 == 0)
   // outputs
   float* e_out;  // blocked (null for the last layer)
   float* h_out;

@@ -673,7 +673,12 @@ __device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t
 
 // Fused layer (large batches): one wave per task runs its 50 edge blocks in order, carrying the
 // ordered segment sums in registers/LDS, then the node update. No per-edge message traffic.
-template <int LAYER>
+// HALF (batches of at most one round of tasks): two waves per task, wave 2t+h running edge
+// blocks 25h .. 25h+24 — exactly receivers 16h .. 16h+15 (800 = 16 x 50 edges), so each half's
+// segment sums are complete on their own; after a workgroup barrier wave 2t runs the node
+// update. The same operations in the same order: identical bits. Every SIMD then holds two
+// waves where a one-wave-per-task round would hold one.
+template <int LAYER, bool HALF>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   __shared__ float lds_scratch[4][64 * 36];
   const int lane = threadIdx.x & 63;
@@ -685,18 +690,21 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (int)(blockIdx.x / 8);
   const int64_t task = (int64_t)wg * 4 + w;
 #else
-  const int64_t task = (int64_t)blockIdx.x * 4 + w;
+  const int64_t task = HALF ? (int64_t)blockIdx.x * 2 + (w >> 1) : (int64_t)blockIdx.x * 4 + w;
 #endif
-  if (task >= a.n_tasks) return;
+  // HALF grids hold exactly n_tasks / 2 workgroups (n_tasks is a multiple of 4): no wave may
+  // leave before the barrier below
+  if (!HALF && task >= a.n_tasks) return;
+  const int blk_lo = HALF ? 25 * (w & 1) : 0, blk_hi = HALF ? blk_lo + 25 : 50;
   const int64_t g0 = task * 32;
   float* scratch = lds_scratch[w];
   float* aggl = a.agg + task * 32 * 128;
   float carry[2] = {0.f, 0.f};  // running sums of the receiver continuing into the next block
 
-  int32_t s_next = edge_sender(a, g0, lane, 0);
-  for (int blk = 0; blk < 50; ++blk) {
+  int32_t s_next = edge_sender(a, g0, lane, blk_lo);
+  for (int blk = blk_lo; blk < blk_hi; ++blk) {
     const int32_t s_cur = s_next;
-    if (blk < 49) s_next = edge_sender(a, g0, lane, blk + 1);
+    if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
     edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m);
     // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order). The
@@ -752,11 +760,20 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
       }
     }
   }
-  // the sums were stored by other lanes of this wave: drain stores, then read back
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // the sums were stored by other lanes of this wave (HALF: and by the partner wave): drain
+  // stores, then read back
+  if (HALF) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (w & 1) return;
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
   // ---------------- node update for the 32 receivers (lane&31 = receiver): the body of
   // node_update, kept inline here — calling the helper makes the compiler spill 45 VGPRs
   // in k_mpnn<1,2> (2 inline).
@@ -1418,9 +1435,16 @@ void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st) {
     else hipLaunchKernelGGL(k_mpnn_node<2>, grid, dim3(256), 0, st, a);
     return;
   }
-  if (layer == 0) hipLaunchKernelGGL(k_mpnn<0>, grid, dim3(256), 0, st, a);
-  else if (layer == 1) hipLaunchKernelGGL(k_mpnn<1>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(k_mpnn<2>, grid, dim3(256), 0, st, a);
+  if (a.half_tasks) {  // two waves per task (n_tasks % 4 == 0: run() pads slots to 128)
+    const dim3 hgrid((unsigned)(a.n_tasks / 2));
+    if (layer == 0) hipLaunchKernelGGL((k_mpnn<0, true>), hgrid, dim3(256), 0, st, a);
+    else if (layer == 1) hipLaunchKernelGGL((k_mpnn<1, true>), hgrid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_mpnn<2, true>), hgrid, dim3(256), 0, st, a);
+    return;
+  }
+  if (layer == 0) hipLaunchKernelGGL((k_mpnn<0, false>), grid, dim3(256), 0, st, a);
+  else if (layer == 1) hipLaunchKernelGGL((k_mpnn<1, false>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((k_mpnn<2, false>), grid, dim3(256), 0, st, a);
 }
 void launch_down(int df, const DownArgs& a, bool coop, hipStream_t st) {
   dim3 grid((unsigned)((a.n_tiles + 3) / 4));

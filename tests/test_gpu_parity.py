@@ -226,11 +226,12 @@ def test_invalid_inputs_rejected():
     assert np.array_equal(tk.tokenize([s])[0], O.tokenize(P.random_blob(6, 1234), LEVELS[4096], 1, s.atom37_positions, s.atom_flags())["tokens"])
 
 
-@pytest.mark.parametrize("split", ["0", "1000000"])
-def test_fused_and_split_layers_identical(split, monkeypatch):
-    """The two MPNN schedules (fused: one wave per 32 receivers; split: edge blocks spread over
-    the GPU, messages through HBM) give the same bits. Small batches default to split, so this
-    forces each mode in a fresh context and compares with the oracle-checked default."""
+@pytest.mark.parametrize("split,half", [("0", "0"), ("0", "1"), ("1000000", "0")])
+def test_fused_and_split_layers_identical(split, half, monkeypatch):
+    """The MPNN schedules (fused: one wave per 32 receivers; fused with two waves per task, 16
+    receivers each; split: edge blocks spread over the GPU, messages through HBM) give the same
+    bits. Small batches default to split, so this forces each mode in a fresh context and
+    compares with the oracle-checked default."""
     from pst_amd._native import Tokenizer, pack_samples
     samples = [synthetic.synthetic_protein(n, 300 + n) for n in (50, 99, 256, 512, 131)]
     pos, flags, off = pack_samples(samples)
@@ -239,6 +240,7 @@ def test_fused_and_split_layers_identical(split, monkeypatch):
     tok2, _, _ = ref.tokenize_packed(pos, flags, off)
     hl2 = [ref.debug_fetch(w, R) for w in (1, 2, 3)]
     monkeypatch.setenv("PST_SPLIT_TASKS", split)
+    monkeypatch.setenv("PST_HALF_TASKS", half)
     monkeypatch.setenv("PST_DEBUG", "1")
     tk = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
     tok, nt, nn = tk.tokenize_packed(pos, flags, off)
