@@ -671,6 +671,9 @@ __device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t
   }
 }
 
+template <int LAYER>
+__device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, int h, float* xs);
+
 // Fused layer (large batches): one wave per task runs its 50 edge blocks in order, carrying the
 // ordered segment sums in registers/LDS, then the node update. No per-edge message traffic.
 // HALF (batches of at most one round of tasks): two waves per task, wave 2t+h running edge
@@ -767,7 +770,10 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (w & 1) return;
+    // the node update on both waves of the pair, two output blocks each, tiles exchanged
+    // through this pair's half of lds_scratch (free after the edge phase)
+    node_update_pair<LAYER>(a, g0, w & 1, lds_scratch[w & 2]);
+    return;
   } else {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_s_waitcnt(0);
@@ -1312,6 +1318,123 @@ __device__ __forceinline__ void blk_store_row(const f32x16& v, float* __restrict
   float4* p = reinterpret_cast<float4*>(row + (lane_id() >> 5) * 64 + w * 16);
 #pragma unroll
   for (int q = 0; q < 4; ++q) p[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+// ------------------------------------------------------------- node_update_pair
+// k_mpnn<L, true>'s node update: wave h of the task's pair computes output blocks 2h and 2h+1 of
+// every GEMM (the block chains of k_mpnn_node_coop, same order, same bits); full tiles are
+// assembled through 16 KB of LDS, single-buffered (a barrier after the writes and after the
+// reads; every wave of the workgroup runs the same sequence).
+__device__ __forceinline__ void pair_exchange(Tile& t, const f32x16& p0, const f32x16& p1, float* xs, int h) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    xs[(2 * h * 16 + r) * 64 + lane] = p0[r];
+    xs[((2 * h + 1) * 16 + r) * 64 + lane] = p1[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t.m[M][r] = xs[(M * 16 + r) * 64 + lane];
+  __syncthreads();
+}
+
+template <int LAYER>
+__device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, int h, float* xs) {
+  const int lane = lane_id();
+  const int b0 = 2 * h, b1 = 2 * h + 1;
+  const int64_t gl = g0 + (lane & 31);
+  Tile x;
+  {
+    f32x16 ag0, ag1;
+    const float* b2 = a.msg.b2 + (lane >> 5) * 64;
+    const float fd = (float)a.deg[gl];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      ag0[r] = fd * b2[b0 * 16 + r];
+      ag1[r] = fd * b2[b1 * 16 + r];
+    }
+    {
+      Tile G;
+      tile_load_perm(G, a.agg + gl * 128);
+      blk_gemm(ag0, G, a.msg.w2, b0);
+      blk_gemm(ag1, G, a.msg.w2, b1);
+    }
+    const float* hrow;
+    if (LAYER == 0) {
+      const int lr = a.node_local[gl];
+      hrow = a.h0tab + (int64_t)(lr < 0 ? 0 : lr) * 128;
+    } else {
+      hrow = a.h_in + gl * 128;
+    }
+    f32x16 xp0 = blk_load_row(hrow, b0), xp1 = blk_load_row(hrow, b1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      xp0[r] = xp0[r] + ag0[r] / 50.0f;
+      xp1[r] = xp1[r] + ag1[r] / 50.0f;
+    }
+    pair_exchange(x, xp0, xp1, xs, h);
+  }
+  tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0
+  f32x16 out0, out1;
+  for (int ck = 0; ck < 4; ++ck) {
+    Tile hid;
+    {
+      f32x16 h0, h1;
+      blk_gemm_bf(h0, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, b0, ActId{});
+      blk_gemm_bf(h1, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, b1, ActId{});
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 v0 = c_gelu2((f32x2){h0[r], h0[r + 1]});
+        const f32x2 v1 = c_gelu2((f32x2){h1[r], h1[r + 1]});
+        h0[r] = v0.x;
+        h0[r + 1] = v0.y;
+        h1[r] = v1.x;
+        h1[r + 1] = v1.y;
+      }
+      pair_exchange(hid, h0, h1, xs, h);
+    }
+    if (ck == 0) {
+      blk_gemm_bf(out0, hid, a.ff_w2, a.ff_bf2, b0, ActId{});
+      blk_gemm_bf(out1, hid, a.ff_w2, a.ff_bf2, b1, ActId{});
+    } else {
+      blk_gemm(out0, hid, a.ff_w2 + ck * 64 * 64, b0);
+      blk_gemm(out1, hid, a.ff_w2 + ck * 64 * 64, b1);
+    }
+  }
+  {
+    f32x16 xp0 = blk_pick(x, b0), xp1 = blk_pick(x, b1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      xp0[r] = xp0[r] + out0[r];
+      xp1[r] = xp1[r] + out1[r];
+    }
+    pair_exchange(x, xp0, xp1, xs, h);
+  }
+  tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
+  blk_store_row(blk_pick(x, b0), a.h_out + gl * 128, b0);
+  blk_store_row(blk_pick(x, b1), a.h_out + gl * 128, b1);
+  if (a.P_out) {
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+      f32x16 pr0, pr1;
+      if (p & 1) {
+        blk_gemm_bf(pr0, x, a.proj_w + p * 64 * 64, a.proj_bf[p >> 1], b0, ActId{});
+        blk_gemm_bf(pr1, x, a.proj_w + p * 64 * 64, a.proj_bf[p >> 1], b1, ActId{});
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          pr0[r] = 0.0f;
+          pr1[r] = 0.0f;
+        }
+        blk_gemm(pr0, x, a.proj_w + p * 64 * 64, b0);
+        blk_gemm(pr1, x, a.proj_w + p * 64 * 64, b1);
+      }
+      blk_store_row(pr0, a.P_out + gl * 512 + p * 128, b0);
+      blk_store_row(pr1, a.P_out + gl * 512 + p * 128, b1);
+    }
+  }
 }
 
 template <int LAYER>

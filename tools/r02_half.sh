@@ -10,8 +10,8 @@ for round in 1 2; do
   unset PST_LIB PST_SPLIT_TASKS PST_HALF_TASKS
   run 128 half >> gpurun_out/${TAG}_ab.txt
   PST_LIB=build/var_old/libpst.so run 128 old >> gpurun_out/${TAG}_ab.txt
-  PST_SPLIT_TASKS=1000000 run 128 split >> gpurun_out/${TAG}_ab.txt
-  PST_SPLIT_TASKS=0 PST_HALF_TASKS=0 run 128 fused1 >> gpurun_out/${TAG}_ab.txt
+
+
   run 1024 half_build >> gpurun_out/${TAG}_ab.txt
   PST_LIB=build/var_old/libpst.so run 1024 old >> gpurun_out/${TAG}_ab.txt
 done
