@@ -1,7 +1,8 @@
 // Diagnostic: the shader clock over time, sampled by one wave on its own stream while other work
 // runs. Sample i = (s_memtime, s_memrealtime) after ~`sleep_units` x 64 x 127 idle cycles; the
 // clock between samples is d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS).
-// The wave exits after n samples.
+// The wave exits after n samples. Build: hipcc --offload-arch=gfx950 -O2 -shared -fPIC
+// clockprobe.hip -o libclockprobe.so (tools/clock_probe.py loads it).
 #include <hip/hip_runtime.h>
 
 __global__ void k_clock_probe(unsigned long long* out, int n, int sleep_units) {
