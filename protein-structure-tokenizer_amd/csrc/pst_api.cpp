@@ -59,11 +59,13 @@ constexpr int64_t SPLIT_EDGE_WAVES = 0;
 // k = ceil(tasks / SIMDs) (use_split_schedule), so every chunk but the last holds a whole number
 // of those rounds — cutting anywhere else adds a round per chunk (bench, 8 192 tasks: an even
 // 1:4 split cost 59.2 vs 52.3 ms device-resident). The first chunk is H2D_FIRST_ROUNDS rounds
-// (its copy is the only exposed one); each next chunk is at most H2D_GROWTH times the previous
-// (the copy runs ~12x faster than the compute, so chunk k+1's copy hides under chunk k). No
-// pipeline below H2D_MIN_ROUNDS rounds in all.
+// (its copy is the only exposed one; one round runs two waves per task, use_half_tasks); each
+// next chunk is at most H2D_GROWTH times the previous (the copy runs ~12x faster than the
+// compute, so chunk k+1's copy hides under chunk k). No pipeline below H2D_MIN_ROUNDS rounds in
+// all. Measured at 8 rounds (tools/r02_first.sh): chunks of 1+7 rounds 54.0-54.2 ms, 2+6
+// 54.9-55.0, 3+5 56.1-56.8, 1+3+4 54.9-55.3, 1+2+4+1 55.2-55.8.
 constexpr int H2D_MAX_CHUNKS = 8;
-constexpr int64_t H2D_FIRST_ROUNDS = 2;
+constexpr int64_t H2D_FIRST_ROUNDS = 1;
 constexpr int64_t H2D_GROWTH = 8;
 constexpr int64_t H2D_MIN_ROUNDS = 4;
 
@@ -234,6 +236,8 @@ struct pst_ctx {
   hipStream_t copy_stream = nullptr;
   hipEvent_t copy_ev[8] = {};
   int64_t h2d_chunks = -2;  // PST_H2D_CHUNKS: force the chunk count (1 = no pipeline); -1 = policy
+  int64_t h2d_first = -2;   // PST_H2D_FIRST_ROUNDS: rounds in the first pipelined chunk; -1 = H2D_FIRST_ROUNDS
+  int64_t h2d_growth = -2;  // PST_H2D_GROWTH: chunk-size growth factor; -1 = H2D_GROWTH
   bool chunked_last = false; // last call was pipelined: per-layer debug intermediates hold its last chunk only
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
@@ -866,7 +870,9 @@ std::vector<int32_t> plan_chunks(pst_ctx* ctx, const int64_t* offsets, int32_t n
   }
   const int64_t round = std::max<int64_t>(1, ctx->n_simds);
   if (tasks >= H2D_MIN_ROUNDS * round) {
-    int64_t want = H2D_FIRST_ROUNDS;  // rounds in the next chunk
+    env_threshold(ctx->h2d_first, "PST_H2D_FIRST_ROUNDS");
+    env_threshold(ctx->h2d_growth, "PST_H2D_GROWTH");
+    int64_t want = ctx->h2d_first > 0 ? ctx->h2d_first : H2D_FIRST_ROUNDS;  // rounds in the next chunk
     int32_t b = 0;
     while ((int)cut.size() < H2D_MAX_CHUNKS) {
       const int64_t r0 = offsets[b];
@@ -877,7 +883,7 @@ std::vector<int32_t> plan_chunks(pst_ctx* ctx, const int64_t* offsets, int32_t n
       if (e == b) break;
       cut.push_back(e);
       b = e;
-      want *= H2D_GROWTH;
+      want *= ctx->h2d_growth > 0 ? ctx->h2d_growth : H2D_GROWTH;
     }
   }
   cut.push_back(n_prot);
