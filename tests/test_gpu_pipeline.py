@@ -47,3 +47,21 @@ def test_chunked_h2d_is_bitwise_identical(cb, df):
         assert np.array_equal(o[4]["argmin"], base[4]["argmin"])
         assert np.array_equal(o[4]["histogram"], base[4]["histogram"])
         assert np.array_equal(o[4]["distances"].view(np.uint32), base[4]["distances"].view(np.uint32))
+
+
+def test_default_pipeline_policy_matches_one_shot():
+    """The bench-sized path as it runs by default: 512 proteins x 256 residues = 4 rounds of
+    tasks, pipelined as a one-round first chunk (two waves per task) and a three-round rest
+    (one wave per task), against one unpipelined call: same token ids and counts."""
+    from pst_amd._native import Tokenizer
+    samples = synthetic.synthetic_batch(512, 256, seed=4242)
+    pos, flags, off = pack_samples(samples)
+    os.environ.pop("PST_H2D_CHUNKS", None)
+    t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
+    tok, nt, nn = t.tokenize_packed(pos, flags, off)
+    t.close()
+    t1 = _ctx(1)
+    tok1, nt1, nn1 = t1.tokenize_packed(pos, flags, off)
+    t1.close()
+    os.environ.pop("PST_H2D_CHUNKS")
+    assert np.array_equal(tok, tok1) and np.array_equal(nt, nt1) and np.array_equal(nn, nn1)
