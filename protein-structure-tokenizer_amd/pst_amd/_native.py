@@ -269,9 +269,11 @@ class Tokenizer:
         offsets = np.ascontiguousarray(offsets, np.int64)
         B = len(offsets) - 1
         R = int(offsets[-1])
-        tok = np.zeros(max(R, 1), np.uint32)
-        nt = np.zeros(B, np.int32)
-        nn = np.zeros(B, np.int32)
+        # every element is written by the call's device-to-host copies (rows past a protein's
+        # n_tokens hold unspecified values, as the reference's padded outputs do)
+        tok = np.empty(max(R, 1), np.uint32)
+        nt = np.empty(B, np.int32)
+        nn = np.empty(B, np.int32)
         self._check(lib().pst_tokenize(self._h, _ptr(pos), _ptr(flags), _ptr(offsets), B, _ptr(tok), _ptr(nt), _ptr(nn)))
         return tok, nt, nn
 
