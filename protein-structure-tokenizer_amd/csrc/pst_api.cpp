@@ -26,7 +26,10 @@ constexpr int KNN = 50;
 // k = ceil(tasks / SIMDs): about k·SIMDs task-units for k >= 2 and 1.1·SIMDs for k = 1 (one
 // wave per SIMD runs alone). The split schedule costs about 1.1 units per task (message rows
 // through HBM). Split wins below ~1 000 tasks and in the half-empty rounds above.
-constexpr double SPLIT_COST_PER_TASK = 1.05;  // one edge block per wave (re-measured, tools/policy_check.sh)
+// 1.05 measured below ~1 000 tasks (tools/policy_check.sh); at 7 680 tasks (960 proteins, the
+// last fused round 3/4 full) the split layers ran 49.98 ms against 48.2 ms for the fused layers
+// of 8 192 tasks — 1.10 per task (profiles/r02_tail_and_policy.txt) — so 1.1
+constexpr double SPLIT_COST_PER_TASK = 1.1;
 constexpr double FUSED_SINGLE_ROUND = 1.1;
 // A single round more than half full runs the fused layers with two waves per task
 // (use_half_tasks): both wave slots of every SIMD busy, about one round of full-size cost plus
