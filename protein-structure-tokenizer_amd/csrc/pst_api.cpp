@@ -70,7 +70,7 @@ constexpr int64_t SPLIT_EDGE_WAVES = 0;
 constexpr int H2D_MAX_CHUNKS = 8;
 constexpr int64_t H2D_FIRST_ROUNDS = 1;
 constexpr int64_t H2D_GROWTH = 8;
-constexpr int64_t H2D_MIN_ROUNDS = 4;
+constexpr int64_t H2D_MIN_ROUNDS = 2;  // 2 / 3 rounds: 15.2-15.3 -> 14.9-15.0 / 22.4-22.7 -> 21.2-21.4 ms
 
 // Schedule thresholds from the environment, read once per context: -2 = not read yet, -1 = unset
 // (use the cost model), >= 0 = the override.
@@ -241,6 +241,7 @@ struct pst_ctx {
   int64_t h2d_chunks = -2;  // PST_H2D_CHUNKS: force the chunk count (1 = no pipeline); -1 = policy
   int64_t h2d_first = -2;   // PST_H2D_FIRST_ROUNDS: rounds in the first pipelined chunk; -1 = H2D_FIRST_ROUNDS
   int64_t h2d_growth = -2;  // PST_H2D_GROWTH: chunk-size growth factor; -1 = H2D_GROWTH
+  int64_t h2d_min = -2;     // PST_H2D_MIN_ROUNDS: no pipeline below this many rounds; -1 = H2D_MIN_ROUNDS
   bool chunked_last = false; // last call was pipelined: per-layer debug intermediates hold its last chunk only
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
@@ -872,7 +873,8 @@ std::vector<int32_t> plan_chunks(pst_ctx* ctx, const int64_t* offsets, int32_t n
     return cut;
   }
   const int64_t round = std::max<int64_t>(1, ctx->n_simds);
-  if (tasks >= H2D_MIN_ROUNDS * round) {
+  env_threshold(ctx->h2d_min, "PST_H2D_MIN_ROUNDS");
+  if (tasks >= (ctx->h2d_min > 0 ? ctx->h2d_min : H2D_MIN_ROUNDS) * round) {
     env_threshold(ctx->h2d_first, "PST_H2D_FIRST_ROUNDS");
     env_threshold(ctx->h2d_growth, "PST_H2D_GROWTH");
     int64_t want = ctx->h2d_first > 0 ? ctx->h2d_first : H2D_FIRST_ROUNDS;  // rounds in the next chunk
