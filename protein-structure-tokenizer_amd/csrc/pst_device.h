@@ -405,6 +405,54 @@ __device__ __forceinline__ void tile_gemm_f(Tile& acc, const Tile& X, const floa
   }
 }
 
+// tile_gemm_f with the fragments of k-steps 0 .. KL-1 read from LDS (`Wl`, staged once per
+// workgroup) and the rest streamed from `Wf` as usual: the same operands and MFMA chain, same bits.
+template <int KL, typename F>
+__device__ __forceinline__ void tile_gemm_mix_f(Tile& acc, const Tile& X, const float4* Wl,
+                                                const float4* __restrict__ Wf, F&& f) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
+  const int lane = lane_id();
+  const int vo = lane * 16;
+  float4 lr[2], ring[GEMM_DEPTH];
+  lr[0] = Wl[lane];
+  lr[1] = Wl[64 + lane];
+  f32x2 bq[2], bn[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bq[j] = f(2 * j, (f32x2){X.m[0][2 * j], X.m[0][2 * j + 1]});
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = 4 * g + j;
+      float4 a;
+      if (t < KL) {
+        a = lr[t % 2];
+        if (t + 2 < KL) lr[t % 2] = Wl[(t + 2) * 64 + lane];
+      } else {
+        a = ring[(t - KL) % GEMM_DEPTH];
+        if (t + GEMM_DEPTH < 64) ring[(t - KL) % GEMM_DEPTH] = buf_load4(rs, vo, (t + GEMM_DEPTH) * 1024);
+      }
+      // the global stream starts GEMM_DEPTH k-steps before the LDS part ends
+      if (t == KL - GEMM_DEPTH) {
+#pragma unroll
+        for (int i = 0; i < GEMM_DEPTH; ++i) ring[i] = buf_load4(rs, vo, (KL + i) * 1024);
+      }
+      if (g < 15 && (j & 1) == 0) {
+        const int u = t + 4;
+        bn[j >> 1] = f(u, (f32x2){X.m[u / 16][u % 16], X.m[u / 16][u % 16 + 1]});
+      }
+      const float b = (j & 1) ? bq[j >> 1].y : bq[j >> 1].x;
+      acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b, acc.m[0], 0, 0, 0);
+      acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b, acc.m[1], 0, 0, 0);
+      acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b, acc.m[2], 0, 0, 0);
+      acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b, acc.m[3], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bq[0] = bn[0];
+    bq[1] = bn[1];
+  }
+}
+
 // acc = bias + X·W: the bias enters as an extra leading k-step (A = bias fragment, lane half 0
 // holds b[32M + (lane&31)], half 1 zeros; B = 1 on half 0, 0 on half 1), so the chain starts
 // from exactly b without a VALU add or a 64-register bias tile.
@@ -420,6 +468,19 @@ __device__ __forceinline__ void tile_gemm_bf(Tile& acc, const Tile& X, const flo
   acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.z, one, z, 0, 0, 0);
   acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.w, one, z, 0, 0, 0);
   tile_gemm_f(acc, X, Wf, f);
+}
+template <int KL, typename F>
+__device__ __forceinline__ void tile_gemm_mix_bf(Tile& acc, const Tile& X, const float4* Wl, const float4* __restrict__ Wf,
+                                                 const float4* __restrict__ Bf, F&& f) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Bf);
+  const float4 bb = buf_load4(rs, lane_id() * 16, 0);
+  const float one = lane_id() < 32 ? 1.0f : 0.0f;
+  const f32x16 z = {};
+  acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.x, one, z, 0, 0, 0);
+  acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.y, one, z, 0, 0, 0);
+  acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.z, one, z, 0, 0, 0);
+  acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(bb.w, one, z, 0, 0, 0);
+  tile_gemm_mix_f<KL>(acc, X, Wl, Wf, f);
 }
 
 // Activation functors: f(t, {x_t, x_t+1}) -> B operands of k-steps t, t+1.

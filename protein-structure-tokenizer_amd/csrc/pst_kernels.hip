@@ -484,9 +484,27 @@ __device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
 // The message MLP up to its last (linear) layer: acc <- GELU(b1 + GELU(acc)·W1). The last layer
 // commutes with the segment sum, sum_j (g_j·W2 + b2) = (sum_j g_j)·W2 + deg·b2, so it runs once
 // per receiver (agg_from_gsum) instead of once per edge.
-__device__ __forceinline__ void msg_hidden(Tile& acc, const MlpW& W) {
+// k-steps of the message MLP's W1 the fused kernels hold in LDS (fragments of k-steps 0 .. KL-1,
+// 1 KB each, read by the workgroup's four waves instead of streamed from L2 every block): layer 0
+// 40 (W1 is most of its weight stream), layers 1-2 32; 2 workgroups per CU still fit (36 KB of
+// segment-sum scratch + 32 / 40 KB). Measured at 1 024 x 256 residues (profiles/r02_ab_w1_lds.txt):
+// k_mpnn<0> 8.50-8.56 (none) -> 8.36-8.40 (32) -> 8.24-8.29 ms (40); layers 1-2 unchanged.
+#ifndef W1_LDS_KSTEPS
+#define W1_LDS_KSTEPS 32
+#endif
+#ifndef W1_LDS_KSTEPS_L0
+#define W1_LDS_KSTEPS_L0 40
+#endif
+template <int LAYER>
+constexpr int w1_lds_ksteps() { return LAYER == 0 ? W1_LDS_KSTEPS_L0 : W1_LDS_KSTEPS; }
+
+template <int KL = 0>
+__device__ __forceinline__ void msg_hidden(Tile& acc, const MlpW& W, const float4* w1_lds = nullptr) {
   Tile a2;
-  tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu{});
+  if (KL > 0 && w1_lds)
+    tile_gemm_mix_bf<(KL > 0 ? KL : 1)>(a2, acc, w1_lds, W.w1, W.bf1, ActGelu{});
+  else
+    tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu{});
   __builtin_amdgcn_sched_barrier(0);
   // 20 wait states: the packed GELU's asm reads the accumulators the last MFMAs just wrote,
   // and only the compiler's hazard recognizer would otherwise space them
@@ -558,7 +576,7 @@ __device__ __forceinline__ int32_t edge_sender(const MpnnArgs& a, int64_t g0, in
 
 template <int LAYER>
 __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int64_t g0, int lane, int blk,
-                                           int32_t s_pre, Tile& m) {
+                                           int32_t s_pre, Tile& m, const float4* w1_lds = nullptr) {
   const int te = 32 * blk + (lane & 31);
   const int rl = te / 50;
   const int64_t g = g0 + rl;
@@ -614,11 +632,11 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
     tile_add_rows(m, a.PM0 + (int64_t)ls0 * 256 + 0, a.PM0 + (int64_t)lr0 * 256 + 128);
     tile_add_row(m, a.Utab + (int64_t)(ls0 - lr0 + 511) * 128);
     feat_gemm(m, x, a.W_msg0f);
-    msg_hidden(m, a.msg);
+    msg_hidden<w1_lds_ksteps<LAYER>()>(m, a.msg, w1_lds);
   } else {
     tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
     tile_gemm(m, e, a.msg.w0);
-    msg_hidden(m, a.msg);
+    msg_hidden<w1_lds_ksteps<LAYER>()>(m, a.msg, w1_lds);
   }
 }
 
@@ -695,6 +713,15 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 #else
   const int64_t task = HALF ? (int64_t)blockIdx.x * 2 + (w >> 1) : (int64_t)blockIdx.x * 4 + w;
 #endif
+  // the first KL k-steps of the message MLP's W1 fragments (msg_hidden), read by every block of
+  // the workgroup's four waves from LDS instead of L2; filled before any wave may leave
+  constexpr int KL = w1_lds_ksteps<LAYER>();
+  __shared__ float4 w1_lds_buf[(KL > 0 ? KL : 1) * 64];
+  const float4* w1_lds = KL > 0 ? w1_lds_buf : nullptr;
+  if (KL > 0) {
+    for (int i = threadIdx.x; i < KL * 64; i += 256) w1_lds_buf[i] = a.msg.w1[i];
+    __syncthreads();
+  }
   // HALF grids hold exactly n_tasks / 2 workgroups (n_tasks is a multiple of 4): no wave may
   // leave before the barrier below
   if (!HALF && task >= a.n_tasks) return;
@@ -709,7 +736,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     const int32_t s_cur = s_next;
     if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
-    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m);
+    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m, w1_lds);
     // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order). The
     // block holds edges of two receivers: rA (block edges 0..lastA) and rA+1 (the rest).
     // Transpose through LDS two accumulator blocks at a time, so that lane l owns channel
