@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--weak", action="store_true", help="every GPU runs --proteins proteins of its own")
     ap.add_argument("--codebook", type=int, default=CODEBOOK, help="secondary configs (default: the metric's 4096)")
     ap.add_argument("--df", type=int, default=DF)
+    ap.add_argument("--f64-input", action="store_true",
+                    help="time pst_tokenize on float64 positions instead of pst_tokenize_f32 on float32 ones")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the CASP14 end-to-end field")
     ap.add_argument("--cpu-sample", type=int, default=8, help="proteins in the reference-as-computed CPU sample")
@@ -331,7 +333,14 @@ def main():
     R = int(off[-1])
     pin_pos = torch.from_numpy(pos).pin_memory()
     pin_flags = torch.from_numpy(flags).pin_memory()
-    ppos, pflags = pin_pos.numpy(), pin_flags.numpy()
+    # the wire format of the timed region: the PDB path's float32 coordinates (pst_tokenize_f32,
+    # 481 B per residue) unless --f64-input (pst_tokenize, 925 B); the generator's values are
+    # float32-exact, so both give the same tokens (checked below)
+    pos32 = pos.astype(np.float32)
+    assert np.array_equal(pos32.astype(np.float64), pos), "synthetic coordinates are not float32-exact"
+    pin_pos32 = torch.from_numpy(pos32).pin_memory()
+    ppos64, pflags = pin_pos.numpy(), pin_flags.numpy()
+    ppos = ppos64 if args.f64_input else pin_pos32.numpy()
     levels = LEVELS[args.codebook]
     blob = P.random_blob(len(levels), 1234)
     tk = Tokenizer(gpu, args.codebook, args.df, blob)
@@ -365,6 +374,20 @@ def main():
     job_res = int(total_res.item())
     med = float(np.median(step_s))
     value = job_res / med
+
+    # the other wire format on the same inputs: same tokens, and its host-to-host time (median of 5)
+    alt = ppos64 if not args.f64_input else pin_pos32.numpy()
+    alt_t = []
+    for i in range(6):
+        t0 = time.perf_counter()
+        tok_alt, _, _ = tk.tokenize_packed(alt, pflags, off)
+        if i:
+            alt_t.append(time.perf_counter() - t0)
+    alt_med = float(np.median(alt_t))
+    other_input = {"input": "float64 (pst_tokenize)" if not args.f64_input else "float32 (pst_tokenize_f32)",
+                   "residues_per_s_per_gpu": round(R / alt_med, 1), "ms": round(alt_med * 1e3, 3),
+                   "tokens_identical": bool(np.array_equal(tok_alt[:R], tok[:R])),
+                   "note": "rank 0's shard, median of 5 after one warm-up"}
 
     # exact match vs the reference fixtures of the proteins this rank holds (summed over ranks)
     ref_match = reference_exact_match(args, ids, tok, off)
@@ -465,8 +488,11 @@ def main():
                        "proteins_job": args.proteins * (world if args.weak else 1), "residues_job": job_res,
                        "proteins_rank0": len(ids), "parallelism": f"dp{world} (independent proteins, LPT shard)",
                        "world_size_seen": seen_world, "dist_backend": args.dist_backend if world > 1 else None},
-            "timed_region": "pinned host atom37 -> H2D -> graph -> encoder -> FSQ -> D2H token ids (pst_tokenize), "
-                            "median over steps of the max over ranks",
+            "timed_region": ("pinned host atom37 -> H2D -> graph -> encoder -> FSQ -> D2H token ids ("
+                             + ("pst_tokenize, float64 positions" if args.f64_input else
+                                "pst_tokenize_f32, float32 positions as the PDB path holds them")
+                             + "), median over steps of the max over ranks"),
+            "other_input_format": other_input,
             "ms_per_step_mean_bracketed": round(elapsed / args.steps * 1e3, 3),
             "elapsed_s": round(elapsed, 3),
             "device_resident": {"residues_per_s_per_gpu": round(R / float(np.median(dts)), 1),

@@ -109,6 +109,17 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
                  int32_t* n_tokens_out, int32_t* n_nodes_out);
 
 /*
+ * pst_tokenize with float32 atom positions [R,37,3]: the PDB path's coordinates are float32
+ * values (Biopython's atom.coord; protein_structure_sample.py:166-248 stores them in float64
+ * arrays), so this is the same input in half the H2D bytes. k_prep widens each value to
+ * float64 on load: for float32-exact coordinates the results are bit-identical to
+ * pst_tokenize's. Same arguments, errors and outputs otherwise.
+ */
+int pst_tokenize_f32(pst_ctx* ctx, const float* atom_pos, const uint8_t* atom_flags,
+                     const int64_t* prot_offsets, int32_t n_prot, uint32_t* tokens_out,
+                     int32_t* n_tokens_out, int32_t* n_nodes_out);
+
+/*
  * Same on device buffers (d_* in HBM of ctx's device), asynchronous on ctx's stream.
  * prot_offsets stays a HOST array (it sizes the launch). Outputs are device buffers with the
  * layout of pst_tokenize; d_n_nodes_out is required (the graph build writes it), d_n_tokens_out

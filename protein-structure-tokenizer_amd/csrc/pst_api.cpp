@@ -521,8 +521,10 @@ int upload_batch_meta(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot, int3
 // One batch (or one chunk of a pipelined batch) through graph → encoder → downsampler/FSQ on
 // ctx->stream. `out_row0`: raw residue row of offsets[0] in the caller's batch, where the
 // raw-layout aux outputs (bounded, quantize, pre_proj) of this batch go.
+// `d_pos32`: float32 positions (pst_tokenize_f32), read by k_prep instead of d_pos when set.
 int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t* offsets, int32_t n_prot,
-        uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes, bool graph_only = false, int64_t out_row0 = 0) {
+        uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes, bool graph_only = false, int64_t out_row0 = 0,
+        const float* d_pos32 = nullptr) {
   const int64_t R = offsets[n_prot];
   int rc = ensure_workspace(ctx, R, n_prot);
   if (rc) return rc;
@@ -537,7 +539,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   HIPCHK(hipMemsetAsync(w.node_prot, 0, sizeof(int32_t) * Rpad, st));
 
   mark(ctx, 0);
-  pst::PrepArgs pa{d_pos, d_flags, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca};
+  pst::PrepArgs pa{d_pos, d_flags, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, d_pos32};
   pst::launch_prep(pa, n_prot, st);
   mark(ctx, 1);
   pst::KnnArgs ka{Rpad, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, w.senders, w.deg, w.feat};
@@ -895,12 +897,10 @@ std::vector<int32_t> plan_chunks(pst_ctx* ctx, const int64_t* offsets, int32_t n
   return cut;
 }
 
-}  // namespace
-
-extern "C" {
-
-int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,
-                 int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
+// pst_tokenize / pst_tokenize_f32: `atom_pos` holds [R,37,3] doubles, or floats when `f32`
+// (copied as they are — half the H2D bytes — and widened to f64 on load in k_prep).
+int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* atom_flags, const int64_t* offsets,
+                  int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
   if (!ctx) return PST_E_INVALID;
   ctx->err.clear();
   if (!atom_pos || !atom_flags || !tokens_out) return fail(ctx, PST_E_INVALID, "null host buffer");
@@ -911,12 +911,18 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
   rc = ensure_workspace(ctx, R, n_prot);
   if (rc) return rc;
   auto& w = ctx->w;
+  // device copy of the positions: w.pos (sized for doubles) holds the floats in its first half
+  const size_t es = f32 ? sizeof(float) : sizeof(double);
+  char* d_pos_bytes = reinterpret_cast<char*>(w.pos);
+  const char* h_pos_bytes = static_cast<const char*>(atom_pos);
+  auto pos64 = [&](int64_t r0) { return f32 ? nullptr : w.pos + 111 * r0; };
+  auto pos32 = [&](int64_t r0) { return f32 ? reinterpret_cast<const float*>(d_pos_bytes) + 111 * r0 : nullptr; };
   const std::vector<int32_t> cut = plan_chunks(ctx, offsets, n_prot);
   const int n_chunks = (int)cut.size() - 1;
   if (n_chunks == 1) {
-    HIPCHK(hipMemcpyAsync(w.pos, atom_pos, sizeof(double) * 111 * R, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(d_pos_bytes, h_pos_bytes, es * 111 * R, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(w.flags, atom_flags, 37 * R, hipMemcpyHostToDevice, ctx->stream));
-    rc = run(ctx, w.pos, w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes);
+    rc = run(ctx, pos64(0), w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes, false, 0, pos32(0));
     if (rc) return rc;
   } else {
     // copy chunk k on copy_stream, then queue its compute behind an event; the host issues
@@ -929,7 +935,7 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
     for (int k = 0; k < n_chunks; ++k) {
       const int32_t b0 = cut[k], b1 = cut[k + 1];
       const int64_t r0 = offsets[b0], r1 = offsets[b1];
-      HIPCHK(hipMemcpyAsync(w.pos + 111 * r0, atom_pos + 111 * r0, sizeof(double) * 111 * (r1 - r0),
+      HIPCHK(hipMemcpyAsync(d_pos_bytes + es * 111 * r0, h_pos_bytes + es * 111 * r0, es * 111 * (r1 - r0),
                             hipMemcpyHostToDevice, ctx->copy_stream));
       HIPCHK(hipMemcpyAsync(w.flags + 37 * r0, atom_flags + 37 * r0, 37 * (r1 - r0), hipMemcpyHostToDevice,
                             ctx->copy_stream));
@@ -937,8 +943,8 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
       HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->copy_ev[k], 0));
       loc.assign(offsets + b0, offsets + b1 + 1);
       for (auto& o : loc) o -= r0;
-      rc = run(ctx, w.pos + 111 * r0, w.flags + 37 * r0, loc.data(), b1 - b0, w.tokens + r0, w.n_tok + b0,
-               w.n_nodes + b0, false, r0);
+      rc = run(ctx, pos64(r0), w.flags + 37 * r0, loc.data(), b1 - b0, w.tokens + r0, w.n_tok + b0,
+               w.n_nodes + b0, false, r0, pos32(r0));
       if (rc) return rc;
     }
     // the batch as a whole for pst_aux / pst_codebook_aux: offsets, token tiles and last_* of all
@@ -962,6 +968,20 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
     HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return PST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,
+                 int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
+  return tokenize_host(ctx, atom_pos, false, atom_flags, offsets, n_prot, tokens_out, n_tokens_out, n_nodes_out);
+}
+
+int pst_tokenize_f32(pst_ctx* ctx, const float* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,
+                     int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
+  return tokenize_host(ctx, atom_pos, true, atom_flags, offsets, n_prot, tokens_out, n_tokens_out, n_nodes_out);
 }
 
 int pst_build_graph(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,

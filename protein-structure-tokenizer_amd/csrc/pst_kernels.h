@@ -15,6 +15,7 @@ struct PrepArgs {
   double* frame;           // [R_pad,9] rows n,u,v
   double* cen;             // [R_pad,3]
   double* ca;              // [R_pad,3]
+  const float* pos32;      // [R,37,3] float32 positions (pst_tokenize_f32); when set, read instead of pos
 };
 
 struct KnnArgs {

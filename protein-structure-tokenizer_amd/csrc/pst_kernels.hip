@@ -91,23 +91,30 @@ __global__ __launch_bounds__(512) void k_prep(PrepArgs a) {
   if (tid == 0) a.n_nodes[b] = total;
   if (keep) {
     const int64_t slot = off + loc;
-    const double* P = a.pos + (off + tid) * NATOM * 3;
+    // positions widened to f64 on load: float32 inputs (pst_tokenize_f32) give the same doubles the
+    // f64 path reads for float32-exact coordinates, so everything below is bitwise unchanged
+    const int64_t p0 = (off + tid) * NATOM * 3;
+    auto P = [&](int i) -> double { return a.pos32 ? (double)a.pos32[p0 + i] : a.pos[p0 + i]; };
     const uint8_t* fl = a.flags + (off + tid) * NATOM;
-    make_frame(P + 0, P + 3, P + 6, a.frame + slot * 9);
+    double bb[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) bb[i] = P(i);
+    make_frame(bb + 0, bb + 3, bb + 6, a.frame + slot * 9);
     double sx = 0.0, sy = 0.0, sz = 0.0;
     int cnt = 0;
     for (int at = 0; at < NATOM; ++at)
       if ((fl[at] & 3) == 3) {  // gt_exists & atom_exists (preprocessing.py:72)
-        if (cnt == 0) { sx = P[3 * at]; sy = P[3 * at + 1]; sz = P[3 * at + 2]; }
-        else { sx += P[3 * at]; sy += P[3 * at + 1]; sz += P[3 * at + 2]; }
+        const double x = P(3 * at), y = P(3 * at + 1), z = P(3 * at + 2);
+        if (cnt == 0) { sx = x; sy = y; sz = z; }
+        else { sx += x; sy += y; sz += z; }
         ++cnt;
       }
     a.cen[slot * 3 + 0] = sx / cnt;
     a.cen[slot * 3 + 1] = sy / cnt;
     a.cen[slot * 3 + 2] = sz / cnt;
-    a.ca[slot * 3 + 0] = P[3];
-    a.ca[slot * 3 + 1] = P[4];
-    a.ca[slot * 3 + 2] = P[5];
+    a.ca[slot * 3 + 0] = bb[3];
+    a.ca[slot * 3 + 1] = bb[4];
+    a.ca[slot * 3 + 2] = bb[5];
     a.node_local[slot] = loc;
     a.node_prot[slot] = b;
   }

@@ -34,7 +34,7 @@ class _ModelDesc(ctypes.Structure):
 
 _lib = None
 EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "pst_create_error",
-           "pst_tokenize", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
+           "pst_tokenize", "pst_tokenize_f32", "pst_tokenize_device", "pst_aux", "pst_codebook_aux", "pst_sync",
            "pst_stream", "pst_debug_fetch", "pst_set_timing", "pst_get_timing", "pst_device_count",
            "pst_codebook_aux_device", "pst_pdb_parse_files", "pst_pdb_parse_strings",
            "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free", "pst_write_files",
@@ -74,6 +74,7 @@ def lib():
         L.pst_last_error.argtypes = [P]
         L.pst_create_error.restype = ctypes.c_char_p
         L.pst_tokenize.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
+        L.pst_tokenize_f32.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
         L.pst_tokenize_device.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P]
         L.pst_aux.argtypes = [P, P, P, P]
         L.pst_build_graph.argtypes = [P, P, P, P, ctypes.c_int32, P, P, P, P]
@@ -263,8 +264,11 @@ class Tokenizer:
         return lib().pst_stream(self._h)
 
     def tokenize_packed(self, pos, flags, offsets):
-        """Ragged batch → (tokens [R] uint32 in raw-offset layout, n_tokens [B], n_nodes [B])."""
-        pos = np.ascontiguousarray(pos, np.float64)
+        """Ragged batch → (tokens [R] uint32 in raw-offset layout, n_tokens [B], n_nodes [B]).
+        float32 positions go through pst_tokenize_f32 (half the H2D bytes, same results for the
+        PDB path's float32 coordinates); anything else is passed as float64 (pst_tokenize)."""
+        f32 = isinstance(pos, np.ndarray) and pos.dtype == np.float32
+        pos = np.ascontiguousarray(pos, np.float32 if f32 else np.float64)
         flags = np.ascontiguousarray(flags, np.uint8)
         offsets = np.ascontiguousarray(offsets, np.int64)
         B = len(offsets) - 1
@@ -274,7 +278,8 @@ class Tokenizer:
         tok = np.empty(max(R, 1), np.uint32)
         nt = np.empty(B, np.int32)
         nn = np.empty(B, np.int32)
-        self._check(lib().pst_tokenize(self._h, _ptr(pos), _ptr(flags), _ptr(offsets), B, _ptr(tok), _ptr(nt), _ptr(nn)))
+        fn = lib().pst_tokenize_f32 if f32 else lib().pst_tokenize
+        self._check(fn(self._h, _ptr(pos), _ptr(flags), _ptr(offsets), B, _ptr(tok), _ptr(nt), _ptr(nn)))
         return tok, nt, nn
 
     def tokenize(self, samples) -> List[np.ndarray]:

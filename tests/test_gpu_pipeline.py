@@ -65,3 +65,41 @@ def test_default_pipeline_policy_matches_one_shot():
     t1.close()
     os.environ.pop("PST_H2D_CHUNKS")
     assert np.array_equal(tok, tok1) and np.array_equal(nt, nt1) and np.array_equal(nn, nn1)
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_f32_positions_match_f64(chunks):
+    """pst_tokenize_f32 (float32 positions, widened to f64 in k_prep) vs pst_tokenize on the same
+    float32-exact values as float64: identical token ids, counts and aux outputs. The batch has
+    extra side-chain atoms (centroids over more than the backbone), dropped backbone atoms (gap
+    slots) and one protein left with < 50 residues after filtering (the short-protein branch)."""
+    rng = np.random.default_rng(11)
+    lens = [int(x) for x in rng.integers(52, 400, 12)]
+    samples = [synthetic.synthetic_protein(n, 700 + i) for i, n in enumerate(lens)]
+    pos, flags, off = pack_samples(samples)
+    R = int(off[-1])
+    extra = rng.random(R) < 0.5  # a CB (atom 3) and a CG (atom 5) on half the residues
+    for at in (3, 5):
+        pos[extra, at] = (pos[extra, 1] + rng.normal(scale=1.5, size=(int(extra.sum()), 3))).astype(np.float32)
+        flags[extra, at] = 3
+    gaps = rng.random(R) < 0.03
+    gaps[int(off[2]):int(off[3])] = False
+    flags[gaps, 0] = 0  # missing N: residue dropped
+    short = slice(int(off[2]), int(off[2]) + max(0, lens[2] - 49))
+    flags[short, 1] = 0  # protein 2 keeps 49 residues
+    pos32 = pos.astype(np.float32)
+    assert np.array_equal(pos32.astype(np.float64), pos)
+    t = _ctx(chunks)
+    tok64, nt64, nn64 = t.tokenize_packed(pos, flags, off)
+    aux64 = t.aux(R)
+    tok32, nt32, nn32 = t.tokenize_packed(pos32, flags, off)
+    aux32 = t.aux(R)
+    t.close()
+    os.environ.pop("PST_H2D_CHUNKS")
+    assert nn64[2] == 49
+    assert np.array_equal(nt32, nt64) and np.array_equal(nn32, nn64)
+    for b in range(len(samples)):
+        a = int(off[b])
+        assert np.array_equal(tok32[a:a + nt32[b]], tok64[a:a + nt64[b]]), b
+    for k in ("bounded", "quantize", "pre_proj"):
+        assert np.array_equal(aux32[k].view(np.uint32), aux64[k].view(np.uint32)), k
