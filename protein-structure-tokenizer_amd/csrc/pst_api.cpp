@@ -68,6 +68,10 @@ constexpr int64_t SPLIT_EDGE_WAVES = 0;
 // all. Measured at 8 rounds (tools/r02_first.sh): chunks of 1+7 rounds 54.0-54.2 ms, 2+6
 // 54.9-55.0, 3+5 56.1-56.8, 1+3+4 54.9-55.3, 1+2+4+1 55.2-55.8.
 constexpr int H2D_MAX_CHUNKS = 8;
+// The first chunk's copy is the exposed one: it is issued as H2D_GRAPH_RANGES protein ranges of
+// about equal residues, and each range's k_prep + k_knn start when that range has landed
+// (GraphRanges), so the graph of the first ranges runs under the copy of the later ones.
+constexpr int64_t H2D_GRAPH_RANGES = 4;
 constexpr int64_t H2D_FIRST_ROUNDS = 1;
 constexpr int64_t H2D_GROWTH = 8;
 constexpr int64_t H2D_MIN_ROUNDS = 2;  // 2 / 3 rounds: 15.2-15.3 -> 14.9-15.0 / 22.4-22.7 -> 21.2-21.4 ms
@@ -242,6 +246,9 @@ struct pst_ctx {
   int64_t h2d_first = -2;   // PST_H2D_FIRST_ROUNDS: rounds in the first pipelined chunk; -1 = H2D_FIRST_ROUNDS
   int64_t h2d_growth = -2;  // PST_H2D_GROWTH: chunk-size growth factor; -1 = H2D_GROWTH
   int64_t h2d_min = -2;     // PST_H2D_MIN_ROUNDS: no pipeline below this many rounds; -1 = H2D_MIN_ROUNDS
+  int64_t h2d_ranges = -2;  // PST_H2D_GRAPH_RANGES: copy ranges of the first chunk (1 = one copy); -1 = H2D_GRAPH_RANGES
+  hipEvent_t range_ev[8] = {};  // one per copy range of the first chunk (GraphRanges)
+  hipEvent_t idle_ev = nullptr; // recorded on `stream` before copy_stream overwrites the inputs
   bool chunked_last = false; // last call was pipelined: per-layer debug intermediates hold its last chunk only
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
@@ -521,10 +528,19 @@ int upload_batch_meta(pst_ctx* ctx, const int64_t* offsets, int32_t n_prot, int3
 // One batch (or one chunk of a pipelined batch) through graph → encoder → downsampler/FSQ on
 // ctx->stream. `out_row0`: raw residue row of offsets[0] in the caller's batch, where the
 // raw-layout aux outputs (bounded, quantize, pre_proj) of this batch go.
+// Protein sub-ranges of one run() whose inputs land separately (pst_tokenize's H2D pipeline):
+// the graph kernels of range k (proteins cut[k] .. cut[k+1]-1) wait for ev[k] only, so they run
+// while the copies of the later ranges are still in flight.
+struct GraphRanges {
+  int n;
+  const int32_t* cut;  // [n+1], cut[0] = 0, cut[n] = n_prot
+  const hipEvent_t* ev;
+};
+
 // `d_pos32`: float32 positions (pst_tokenize_f32), read by k_prep instead of d_pos when set.
 int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t* offsets, int32_t n_prot,
         uint32_t* d_tokens, int32_t* d_ntok, int32_t* d_nnodes, bool graph_only = false, int64_t out_row0 = 0,
-        const float* d_pos32 = nullptr) {
+        const float* d_pos32 = nullptr, const GraphRanges* ranges = nullptr) {
   const int64_t R = offsets[n_prot];
   int rc = ensure_workspace(ctx, R, n_prot);
   if (rc) return rc;
@@ -539,11 +555,20 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   HIPCHK(hipMemsetAsync(w.node_prot, 0, sizeof(int32_t) * Rpad, st));
 
   mark(ctx, 0);
-  pst::PrepArgs pa{d_pos, d_flags, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, d_pos32};
-  pst::launch_prep(pa, n_prot, st);
-  mark(ctx, 1);
-  pst::KnnArgs ka{Rpad, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, w.senders, w.deg, w.feat};
-  pst::launch_knn(ka, st);
+  // the graph per protein range (one range unless the caller pipelines the copy): k_prep over the
+  // range's proteins, then k_knn over its slots (the last range also takes the padding slots)
+  const int n_ranges = ranges ? ranges->n : 1;
+  for (int k = 0; k < n_ranges; ++k) {
+    const int32_t p0 = ranges ? ranges->cut[k] : 0, p1 = ranges ? ranges->cut[k + 1] : n_prot;
+    if (ranges) HIPCHK(hipStreamWaitEvent(st, ranges->ev[k], 0));
+    pst::PrepArgs pa{d_pos, d_flags, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, d_pos32, p0};
+    pst::launch_prep(pa, p1 - p0, st);
+    if (k == 0) mark(ctx, 1);
+    const int64_t s1 = p1 == n_prot ? Rpad : offsets[p1];
+    pst::KnnArgs ka{s1, w.offsets, d_nnodes, w.node_local, w.node_prot, w.frame, w.cen, w.ca, w.senders, w.deg,
+                    w.feat, offsets[p0]};
+    pst::launch_knn(ka, st);
+  }
   mark(ctx, 2);
   if (graph_only) {  // pst_build_graph: the encoder's outputs of an earlier call are gone
     HIPCHK(hipGetLastError());
@@ -814,6 +839,9 @@ int pst_destroy(pst_ctx* ctx) {
   }
   for (hipEvent_t e : ctx->copy_ev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->range_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->idle_ev) (void)hipEventDestroy(ctx->idle_ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return PST_OK;
@@ -919,34 +947,66 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
   auto pos32 = [&](int64_t r0) { return f32 ? reinterpret_cast<const float*>(d_pos_bytes) + 111 * r0 : nullptr; };
   const std::vector<int32_t> cut = plan_chunks(ctx, offsets, n_prot);
   const int n_chunks = (int)cut.size() - 1;
-  if (n_chunks == 1) {
-    HIPCHK(hipMemcpyAsync(d_pos_bytes, h_pos_bytes, es * 111 * R, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(w.flags, atom_flags, 37 * R, hipMemcpyHostToDevice, ctx->stream));
-    rc = run(ctx, pos64(0), w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes, false, 0, pos32(0));
-    if (rc) return rc;
-  } else {
-    // copy chunk k on copy_stream, then queue its compute behind an event; the host issues
-    // copy k+1 after compute k is queued, so even a staged (pageable) copy overlaps compute k
-    if (!ctx->copy_stream) {
-      HIPCHK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
-      for (int k = 0; k < H2D_MAX_CHUNKS; ++k) HIPCHK(hipEventCreateWithFlags(&ctx->copy_ev[k], hipEventDisableTiming));
-    }
-    std::vector<int64_t> loc;
-    for (int k = 0; k < n_chunks; ++k) {
-      const int32_t b0 = cut[k], b1 = cut[k + 1];
-      const int64_t r0 = offsets[b0], r1 = offsets[b1];
-      HIPCHK(hipMemcpyAsync(d_pos_bytes + es * 111 * r0, h_pos_bytes + es * 111 * r0, es * 111 * (r1 - r0),
-                            hipMemcpyHostToDevice, ctx->copy_stream));
-      HIPCHK(hipMemcpyAsync(w.flags + 37 * r0, atom_flags + 37 * r0, 37 * (r1 - r0), hipMemcpyHostToDevice,
-                            ctx->copy_stream));
+  env_threshold(ctx->h2d_ranges, "PST_H2D_GRAPH_RANGES");
+  const int want_ranges = (int)std::min<int64_t>(8, ctx->h2d_ranges >= 0 ? std::max<int64_t>(1, ctx->h2d_ranges)
+                                                                         : H2D_GRAPH_RANGES);
+  if (!ctx->copy_stream) {
+    HIPCHK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    for (int k = 0; k < H2D_MAX_CHUNKS; ++k) HIPCHK(hipEventCreateWithFlags(&ctx->copy_ev[k], hipEventDisableTiming));
+    for (int k = 0; k < 8; ++k) HIPCHK(hipEventCreateWithFlags(&ctx->range_ev[k], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->idle_ev, hipEventDisableTiming));
+  }
+  // inputs are overwritten on copy_stream only after everything queued on `stream` so far
+  HIPCHK(hipEventRecord(ctx->idle_ev, ctx->stream));
+  HIPCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->idle_ev, 0));
+  auto copy_rows = [&](int64_t r0, int64_t r1) -> int {
+    HIPCHK(hipMemcpyAsync(d_pos_bytes + es * 111 * r0, h_pos_bytes + es * 111 * r0, es * 111 * (r1 - r0),
+                          hipMemcpyHostToDevice, ctx->copy_stream));
+    HIPCHK(hipMemcpyAsync(w.flags + 37 * r0, atom_flags + 37 * r0, 37 * (r1 - r0), hipMemcpyHostToDevice,
+                          ctx->copy_stream));
+    return PST_OK;
+  };
+  // chunk k: copied on copy_stream, its compute queued on `stream` behind the copy's event(s); the
+  // host issues copy k+1 after compute k is queued. The first chunk is copied in protein ranges.
+  std::vector<int64_t> loc;
+  std::vector<int32_t> rcut;
+  for (int k = 0; k < n_chunks; ++k) {
+    const int32_t b0 = cut[k], b1 = cut[k + 1];
+    const int64_t r0 = offsets[b0], r1 = offsets[b1];
+    loc.assign(offsets + b0, offsets + b1 + 1);
+    for (auto& o : loc) o -= r0;
+    GraphRanges gr{0, nullptr, ctx->range_ev};
+    const int nr = k == 0 ? std::min(want_ranges, (int)(b1 - b0)) : 1;
+    if (nr > 1) {
+      // range cuts at protein boundaries, about equal residues each
+      rcut.assign(1, 0);
+      for (int32_t b = 1; b < b1 - b0 && (int)rcut.size() < nr; ++b)
+        if (loc[b] * nr >= (int64_t)rcut.size() * loc[b1 - b0]) rcut.push_back(b);
+      rcut.push_back(b1 - b0);
+      gr.n = (int)rcut.size() - 1;
+      gr.cut = rcut.data();
+      for (int q = 0; q < gr.n; ++q) {
+        rc = copy_rows(r0 + loc[rcut[q]], r0 + loc[rcut[q + 1]]);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(ctx->range_ev[q], ctx->copy_stream));
+      }
+    } else {
+      rc = copy_rows(r0, r1);
+      if (rc) return rc;
       HIPCHK(hipEventRecord(ctx->copy_ev[k], ctx->copy_stream));
       HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->copy_ev[k], 0));
-      loc.assign(offsets + b0, offsets + b1 + 1);
-      for (auto& o : loc) o -= r0;
-      rc = run(ctx, pos64(r0), w.flags + 37 * r0, loc.data(), b1 - b0, w.tokens + r0, w.n_tok + b0,
-               w.n_nodes + b0, false, r0, pos32(r0));
-      if (rc) return rc;
     }
+    if (n_chunks == 1) {
+      rc = run(ctx, pos64(0), w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes, false, 0, pos32(0),
+               gr.n > 1 ? &gr : nullptr);
+      if (rc) return rc;
+      break;
+    }
+    rc = run(ctx, pos64(r0), w.flags + 37 * r0, loc.data(), b1 - b0, w.tokens + r0, w.n_tok + b0, w.n_nodes + b0,
+             false, r0, pos32(r0), gr.n > 1 ? &gr : nullptr);
+    if (rc) return rc;
+  }
+  if (n_chunks > 1) {
     // the batch as a whole for pst_aux / pst_codebook_aux: offsets, token tiles and last_* of all
     // chunks (the chunks' own metadata uploads were stream-ordered before this one)
     int32_t n_tiles = 0;

@@ -16,6 +16,7 @@ struct PrepArgs {
   double* cen;             // [R_pad,3]
   double* ca;              // [R_pad,3]
   const float* pos32;      // [R,37,3] float32 positions (pst_tokenize_f32); when set, read instead of pos
+  int32_t prot0;           // first protein of this launch (one block per protein from prot0)
 };
 
 struct KnnArgs {
@@ -30,6 +31,7 @@ struct KnnArgs {
   int32_t* senders;  // [R_pad*50] global slot of the sender
   int32_t* deg;      // [R_pad] valid slots per receiver
   float* feat;       // [R_pad*50, 32]
+  int64_t slot0;     // first slot of this launch (slots slot0 .. n_slots-1, one wave each)
 };
 
 struct MlpW {  // one 3-layer MLP on the edge tile; w*: A fragments [64][64] float4, b*: perm

@@ -70,7 +70,7 @@ __device__ __forceinline__ void make_frame(const double* N, const double* CA, co
 
 __global__ __launch_bounds__(512) void k_prep(PrepArgs a) {
   __shared__ int wave_cnt[8];
-  const int b = blockIdx.x;
+  const int b = a.prot0 + (int)blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t off = a.offsets[b];
   const int Rb = (int)(a.offsets[b + 1] - off);
@@ -241,7 +241,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
   const int lane = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t g = a.slot0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= a.n_slots) return;
   const int loc = a.node_local[g];
   int32_t* snd = a.senders + g * KNN;
@@ -1568,10 +1568,10 @@ __global__ __launch_bounds__(256) void k_table_gemm(const float* __restrict__ X,
 
 // --------------------------------------------------------------------------- launchers
 void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st) {
-  hipLaunchKernelGGL(k_prep, dim3(n_prot), dim3(512), 0, st, a);
+  if (n_prot > 0) hipLaunchKernelGGL(k_prep, dim3(n_prot), dim3(512), 0, st, a);
 }
 void launch_knn(const KnnArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_knn, dim3((unsigned)((a.n_slots + 3) / 4)), dim3(256), 0, st, a);
+  if (a.n_slots > a.slot0) hipLaunchKernelGGL(k_knn, dim3((unsigned)((a.n_slots - a.slot0 + 3) / 4)), dim3(256), 0, st, a);
 }
 void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st) {
   dim3 grid((unsigned)((a.n_tasks + 3) / 4));

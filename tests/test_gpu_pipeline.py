@@ -1,5 +1,6 @@
 """pst_tokenize's H2D pipeline (protein chunks copied on a second stream while the previous
-chunk computes) gives the same bits as the one-shot call: token ids, n_tokens / n_nodes, the
+chunk computes; the first chunk's copy in protein ranges whose graph kernels start as each range
+lands) gives the same bits as the one-shot call: token ids, n_tokens / n_nodes, the
 aux outputs and the codebook aux (distances, argmin, histogram) over the whole batch."""
 import os
 
@@ -13,10 +14,16 @@ from pst_amd._native import pack_samples
 pytestmark = pytest.mark.gpu
 
 
-def _ctx(chunks, cb=4096, df=1):
+def _ctx(chunks, cb=4096, df=1, ranges=None):
+    """ranges: copy ranges of the first chunk (PST_H2D_GRAPH_RANGES; None = the default 4)."""
     from pst_amd._native import Tokenizer
     os.environ["PST_H2D_CHUNKS"] = str(chunks)  # read at the context's first call
+    if ranges is None:
+        os.environ.pop("PST_H2D_GRAPH_RANGES", None)
+    else:
+        os.environ["PST_H2D_GRAPH_RANGES"] = str(ranges)
     t = Tokenizer(0, cb, df, P.random_blob(6, 1234))
+    os.environ.pop("PST_H2D_GRAPH_RANGES", None)
     return t
 
 
@@ -28,8 +35,10 @@ def test_chunked_h2d_is_bitwise_identical(cb, df):
     pos, flags, off = pack_samples(samples)
     R = int(off[-1])
     outs = []
-    for chunks in (1, 3, 8):
-        t = _ctx(chunks, cb, df)
+    # one copy and one graph launch (the reference point), then the first chunk copied in 4 / 8
+    # protein ranges with the graph per range, at 1, 3 and 8 chunks
+    for chunks, ranges in ((1, 1), (1, None), (1, 8), (3, None), (8, None)):
+        t = _ctx(chunks, cb, df, ranges)
         tok, nt, nn = t.tokenize_packed(pos, flags, off)
         tok2, _, _ = t.tokenize_packed(pos, flags, off)  # a second call on the same context
         aux = t.aux(R)
