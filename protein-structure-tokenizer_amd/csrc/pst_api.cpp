@@ -74,7 +74,11 @@ constexpr int H2D_MAX_CHUNKS = 8;
 constexpr int64_t H2D_GRAPH_RANGES = 4;
 constexpr int64_t H2D_FIRST_ROUNDS = 1;
 constexpr int64_t H2D_GROWTH = 8;
-constexpr int64_t H2D_MIN_ROUNDS = 2;  // 2 / 3 rounds: 15.2-15.3 -> 14.9-15.0 / 22.4-22.7 -> 21.2-21.4 ms
+// With float64 positions 2 / 3 rounds gained from the pipeline (15.2-15.3 -> 14.9-15.0 / 22.4-22.7 ->
+// 21.2-21.4 ms); with the float32 wire format and graph ranges 2 rounds run better unpipelined
+// (256 proteins 14.56 -> 14.31-14.40 ms), 4 rounds still gain (512: 28.09-28.16 -> 27.95-28.05 ms,
+// 1024: 54.8 -> 53.8 ms; profiles/r02_h2d_policy_f32.txt)
+constexpr int64_t H2D_MIN_ROUNDS = 3;
 
 // Schedule thresholds from the environment, read once per context: -2 = not read yet, -1 = unset
 // (use the cost model), >= 0 = the override.
@@ -976,7 +980,11 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
     loc.assign(offsets + b0, offsets + b1 + 1);
     for (auto& o : loc) o -= r0;
     GraphRanges gr{0, nullptr, ctx->range_ev};
-    const int nr = k == 0 ? std::min(want_ranges, (int)(b1 - b0)) : 1;
+    // ranges only for a first chunk of at least half a round of tasks: below that the copy is
+    // short and the extra (pageable-staged) copies and launches cost more than they hide
+    // (CASP14, 176 tasks: tokenize 2.07 -> 2.49 ms with 4 ranges)
+    const bool big = (r1 - r0 + 127) / 128 * 4 >= std::max<int64_t>(1, ctx->n_simds / 2);
+    const int nr = k == 0 && big ? std::min(want_ranges, (int)(b1 - b0)) : 1;
     if (nr > 1) {
       // range cuts at protein boundaries, about equal residues each
       rcut.assign(1, 0);
@@ -998,12 +1006,12 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
     }
     if (n_chunks == 1) {
       rc = run(ctx, pos64(0), w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes, false, 0, pos32(0),
-               gr.n > 1 ? &gr : nullptr);
+               gr.n > 0 ? &gr : nullptr);
       if (rc) return rc;
       break;
     }
     rc = run(ctx, pos64(r0), w.flags + 37 * r0, loc.data(), b1 - b0, w.tokens + r0, w.n_tok + b0, w.n_nodes + b0,
-             false, r0, pos32(r0), gr.n > 1 ? &gr : nullptr);
+             false, r0, pos32(r0), gr.n > 0 ? &gr : nullptr);
     if (rc) return rc;
   }
   if (n_chunks > 1) {

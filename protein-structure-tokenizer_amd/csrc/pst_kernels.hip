@@ -544,8 +544,14 @@ __device__ __forceinline__ void agg_from_gsum(Tile& ag, const float* __restrict_
 // x[r] holds features (r&3) + 8(r>>2) + 4·half (the k order of the fragments)
 // (fragments through a buffer resource with constant SGPR offsets and a FEAT_DEPTH-deep register
 // ring, as tile_gemm_f: no per-k-step 64-bit addresses; k_mpnn<0> 8.60 -> 8.45 ms)
+// k-step 15 holds features 27 and 31, both zero padding (edge_features writes +0.0f there), so
+// it is skipped: its four MFMAs would add +-0 products to the chains (no change to a nonzero sum;
+// FEAT_KSTEPS=16 restores them for A/B)
 #ifndef FEAT_DEPTH
 #define FEAT_DEPTH 4
+#endif
+#ifndef FEAT_KSTEPS
+#define FEAT_KSTEPS 15
 #endif
 __device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const float4* __restrict__ Wf) {
   __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
@@ -554,9 +560,9 @@ __device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const
 #pragma unroll
   for (int i = 0; i < FEAT_DEPTH; ++i) ring[i] = buf_load4(rs, vo, i * 1024);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < FEAT_KSTEPS; ++r) {
     const float4 wa = ring[r % FEAT_DEPTH];
-    if (r + FEAT_DEPTH < 16) ring[r % FEAT_DEPTH] = buf_load4(rs, vo, (r + FEAT_DEPTH) * 1024);
+    if (r + FEAT_DEPTH < FEAT_KSTEPS) ring[r % FEAT_DEPTH] = buf_load4(rs, vo, (r + FEAT_DEPTH) * 1024);
     acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, x[r], acc.m[0], 0, 0, 0);
     acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, x[r], acc.m[1], 0, 0, 0);
     acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, x[r], acc.m[2], 0, 0, 0);

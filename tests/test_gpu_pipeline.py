@@ -112,3 +112,21 @@ def test_f32_positions_match_f64(chunks):
         assert np.array_equal(tok32[a:a + nt32[b]], tok64[a:a + nt64[b]]), b
     for k in ("bounded", "quantize", "pre_proj"):
         assert np.array_equal(aux32[k].view(np.uint32), aux64[k].view(np.uint32)), k
+
+
+def test_two_proteins_small_first():
+    """A two-protein batch whose first protein is the smaller: the range cut leaves one copy
+    range, whose event the graph launch must still wait for (a missing wait raced the copy)."""
+    samples = [synthetic.synthetic_protein(60, 41), synthetic.synthetic_protein(480, 42)]
+    pos, flags, off = pack_samples(samples)
+    outs = []
+    for ranges in (1, None):
+        t = _ctx(1, ranges=ranges)
+        for _ in range(3):
+            outs.append(t.tokenize_packed(pos, flags, off))
+        t.close()
+    os.environ.pop("PST_H2D_CHUNKS")
+    for o in outs[1:]:
+        assert np.array_equal(o[1], outs[0][1]) and np.array_equal(o[2], outs[0][2])
+        assert list(o[2]) == [60, 480]
+        assert np.array_equal(o[0], outs[0][0])
