@@ -5,8 +5,10 @@ df = 1, batch-sharded over the N GPUs of the job (LPT on residues: 128 proteins 
 "scaling": "strong", total work fixed). `--weak` instead gives every GPU its own 1 024 proteins.
 
 One step = BASELINE.md §4's timed region on every rank: atom37 arrays in pinned host memory →
-H2D → graph build → 3 MPNN layers → downsampler → FSQ → D2H token ids (`pst_tokenize`, one
-synchronous call per rank; libpst pipelines the H2D of protein chunks with the compute). W
+H2D → graph build → 3 MPNN layers → downsampler → FSQ → D2H token ids (`pst_tokenize_f32`: the
+float32 coordinates the PDB path holds, widened to float64 on the GPU with identical results;
+`--f64-input` times `pst_tokenize` on float64 arrays, and the other format is reported beside it;
+one synchronous call per rank; libpst pipelines the H2D of protein chunks with the compute). W
 warm-up steps, then K timed steps bracketed by barrier + synchronize; each step is also timed
 on its own, the per-step time is the max over ranks, `ms_per_step` is the median of the K and
 `value` = all residues of the job / that median.
