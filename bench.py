@@ -118,10 +118,26 @@ def spawn_workers(n: int) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    for p in procs:
-        rc = rc or p.wait()
-    return rc
+    # wait for every child; once one fails, the others may be blocked in a collective with it,
+    # so they get a grace period and are then terminated (never left holding a GPU)
+    import time
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        if failed_at is None and any(p.returncode not in (None, 0) for p in procs):
+            failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > 30:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=15)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    codes = [p.wait() for p in procs]
+    return next((c for c in codes if c != 0), 0)
 
 
 def init_group(backend: str, **kw) -> None:

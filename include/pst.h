@@ -203,6 +203,15 @@ const char* pst_decoder_create_error(void);
  * n_nodes_out [B] (may be NULL) receives N_b. */
 int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* token_offsets,
                        int32_t n_prot, float* atom37_out, int32_t* n_nodes_out);
+/* pst_decoder_decode for the autoencoder pass (Vq3D.__call__, model/model.py:194-259, which
+ * InferenceRunner.prepare_ae_fn pmaps, scripts/inference_runner.py:209-222): there the decoder's
+ * nodes_mask is the graph's, so protein b decodes n_nodes_in[b] residues, df·T_b <= n < df·(T_b+1)
+ * (the node count its T_b = floor(n / df) tokens came from, preprocessing.py:212-216); NULL gives
+ * df·T_b as pst_decoder_decode. up_proj_out [sum T_b, 128] (may be NULL) receives
+ * quantize_post_proj = up_proj(codes) of every token, rows laid out like `tokens`. */
+int pst_decoder_decode_ex(pst_decoder* dec, const uint32_t* tokens, const int64_t* token_offsets,
+                          int32_t n_prot, const int32_t* n_nodes_in, float* atom37_out,
+                          int32_t* n_nodes_out, float* up_proj_out);
 /* Intermediates of the last decode call (needs PST_DEBUG=1): which = 0 single [sum N,128],
  * 1 pair [sum N², 128], 2 affine trajectory [per protein 8, N, 7], 3 torsion sin/cos
  * [per protein 8, N, 3, 2], 4 atom14 [sum N, 14, 3]. */
@@ -249,7 +258,9 @@ void* pst_stream(pst_ctx* ctx);
 
 /* Debug: copy an intermediate of the LAST call to host.
  *   which = 0..3: node features after init embed / MPNN layer 1..3, [R,128] (raw slot rows)
- *   which = 10:   edge features [R*k, 32] float (27 used), which = 11: senders [R*k] int32 */
+ *   which = 10:   edge features [R*k, 32] float (27 used), which = 11: senders [R*k] int32
+ *   which = 20:   int32[2] plan of the last pst_tokenize(_f32) call: {copy ranges of its first
+ *                 chunk (0 = one copy, the range branch not taken), pipeline chunks} */
 int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes);
 
 #ifdef __cplusplus

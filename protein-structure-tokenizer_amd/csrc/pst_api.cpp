@@ -254,6 +254,7 @@ struct pst_ctx {
   hipEvent_t range_ev[8] = {};  // one per copy range of the first chunk (GraphRanges)
   hipEvent_t idle_ev = nullptr; // recorded on `stream` before copy_stream overwrites the inputs
   bool chunked_last = false; // last call was pipelined: per-layer debug intermediates hold its last chunk only
+  int32_t last_plan[2] = {0, 0}; // last host call: copy ranges of its first chunk (0 = one copy), chunks (pst_debug_fetch 20)
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
   bool timing = false;
@@ -982,8 +983,9 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
     GraphRanges gr{0, nullptr, ctx->range_ev};
     // ranges only for a first chunk of at least half a round of tasks: below that the copy is
     // short and the extra (pageable-staged) copies and launches cost more than they hide
-    // (CASP14, 176 tasks: tokenize 2.07 -> 2.49 ms with 4 ranges)
-    const bool big = (r1 - r0 + 127) / 128 * 4 >= std::max<int64_t>(1, ctx->n_simds / 2);
+    // (CASP14, 176 tasks: tokenize 2.07 -> 2.49 ms with 4 ranges). An explicit
+    // PST_H2D_GRAPH_RANGES > 1 applies at any size (tests reach the range branch with it).
+    const bool big = (r1 - r0 + 127) / 128 * 4 >= std::max<int64_t>(1, ctx->n_simds / 2) || ctx->h2d_ranges > 1;
     const int nr = k == 0 && big ? std::min(want_ranges, (int)(b1 - b0)) : 1;
     if (nr > 1) {
       // range cuts at protein boundaries, about equal residues each
@@ -1003,6 +1005,10 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
       if (rc) return rc;
       HIPCHK(hipEventRecord(ctx->copy_ev[k], ctx->copy_stream));
       HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->copy_ev[k], 0));
+    }
+    if (k == 0) {
+      ctx->last_plan[0] = nr > 1 ? gr.n : 0;  // 0: one copy, no range branch
+      ctx->last_plan[1] = n_chunks;
     }
     if (n_chunks == 1) {
       rc = run(ctx, pos64(0), w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes, false, 0, pos32(0),
@@ -1232,6 +1238,11 @@ int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t
 
 int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes) {
   if (!ctx || ctx->last_R == 0) return PST_E_INVALID;
+  if (which == 20) {  // the last host call's plan: {copy ranges of its first chunk, chunks}
+    if (bytes < sizeof(ctx->last_plan)) return fail(ctx, PST_E_INVALID, "debug buffer too small");
+    std::memcpy(out, ctx->last_plan, sizeof(ctx->last_plan));
+    return PST_OK;
+  }
   if (ctx->chunked_last)
     return fail(ctx, PST_E_INVALID, "the last call was pipelined in chunks (PST_H2D_CHUNKS=1 keeps intermediates)");
   HIPCHK(hipSetDevice(ctx->device));

@@ -1008,7 +1008,9 @@ inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, i
     // shorter dependent chains (measured on 8 x 256 decodes: four accumulators per wave with 4/16
     // slices 7.05 ms, one with 4/8 slices 6.08 ms)
     auto go = [&](auto kern, int slices) {
-      const int ks = (K / slices + 3) / 4 * 4;
+      // slice width rounded UP (to whole 4-k fragment groups): ks · slices >= K, so no tail of K is
+      // dropped; the last slices may be short or empty (k1 = min(K, k0 + ks) in the kernel)
+      const int ks = ((K + slices - 1) / slices + 3) / 4 * 4;
       dim3 grid((unsigned)((N + 31) / 32), (unsigned)((M + 31) / 32));
       hipLaunchKernelGGL(kern, grid, dim3(64 * slices), 0, st, X, ldx, Wt, N, b, Y, ldy, M, N, K, flags, ks);
     };
@@ -1438,6 +1440,11 @@ const char* pst_decoder_last_error(const pst_decoder* dec) { return dec ? dec->e
 
 int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* token_offsets, int32_t n_prot,
                        float* atom37_out, int32_t* n_nodes_out) {
+  return pst_decoder_decode_ex(dec, tokens, token_offsets, n_prot, nullptr, atom37_out, n_nodes_out, nullptr);
+}
+
+int pst_decoder_decode_ex(pst_decoder* dec, const uint32_t* tokens, const int64_t* token_offsets, int32_t n_prot,
+                          const int32_t* n_nodes_in, float* atom37_out, int32_t* n_nodes_out, float* up_proj_out) {
   if (!dec) return PST_E_INVALID;
   dec->err.clear();
   if (!tokens || !token_offsets || n_prot < 1 || !atom37_out) return dfail(dec, PST_E_INVALID, "null argument");
@@ -1450,6 +1457,14 @@ int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* 
     if (T < 0 || T > max_tok)
       return dfail(dec, PST_E_INVALID, "protein " + std::to_string(b) + ": token count outside [0, " +
                                            std::to_string(max_tok) + "]");
+    if (n_nodes_in) {
+      // the graph's node count n gives T = floor(n / df) tokens (preprocessing.py:212-216)
+      const int64_t n = n_nodes_in[b];
+      if (n < T * dec->df || n >= (T + 1) * dec->df || n > 512 || (T == 0 && n != 0))
+        return dfail(dec, PST_E_INVALID, "protein " + std::to_string(b) + ": " + std::to_string(n) +
+                                             " nodes do not give " + std::to_string(T) + " tokens at df " +
+                                             std::to_string(dec->df));
+    }
   }
   DCHK(hipSetDevice(dec->device));
   Scratch S;
@@ -1469,8 +1484,9 @@ int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* 
     G.node_off.push_back(0);
     G.pair_off.push_back(0);
     const int64_t out0 = out_node;
+    const int b0 = b;
     while (b < n_prot) {
-      const int64_t T = token_offsets[b + 1] - token_offsets[b], N = T * dec->df;
+      const int64_t T = token_offsets[b + 1] - token_offsets[b], N = n_nodes_in ? n_nodes_in[b] : T * dec->df;
       if (G.B > 0 && (G.N + N > kNodeCap || G.NP + N * N > kPairCap)) break;
       if (n_nodes_out) n_nodes_out[b] = (int32_t)N;
       if (T > 0) {  // empty proteins take no rows
@@ -1496,6 +1512,10 @@ int pst_decoder_decode(pst_decoder* dec, const uint32_t* tokens, const int64_t* 
     if (rc) return rc;
     DCHK(hipMemcpyAsync(atom37_out + out0 * 111, S.atom37, sizeof(float) * G.N * 111, hipMemcpyDeviceToHost,
                         dec->stream));
+    if (up_proj_out)  // quantize_post_proj: the up_proj half of each token's [PE | up_proj] row
+      DCHK(hipMemcpy2DAsync(up_proj_out + token_offsets[b0] * 128, 128 * sizeof(float), S.orig_in + 128,
+                            256 * sizeof(float), 128 * sizeof(float), (size_t)G.T, hipMemcpyDeviceToHost,
+                            dec->stream));
     DCHK(hipStreamSynchronize(dec->stream));
   }
   return PST_OK;

@@ -39,7 +39,8 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_codebook_aux_device", "pst_pdb_parse_files", "pst_pdb_parse_strings",
            "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free", "pst_write_files",
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
-           "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_debug", "pst_build_graph")
+           "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_decode_ex", "pst_decoder_debug",
+           "pst_build_graph")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -103,6 +104,7 @@ def lib():
         L.pst_decoder_last_error.argtypes = [P]
         L.pst_decoder_create_error.restype = ctypes.c_char_p
         L.pst_decoder_decode.argtypes = [P, P, P, ctypes.c_int32, P, P]
+        L.pst_decoder_decode_ex.argtypes = [P, P, P, ctypes.c_int32, P, P, P, P]
         L.pst_decoder_debug.argtypes = [P, ctypes.c_int32, P, ctypes.c_size_t]
         _lib = L
     return _lib
@@ -359,6 +361,13 @@ class Tokenizer:
         self._check(lib().pst_debug_fetch(self._h, which, _ptr(out), out.nbytes))
         return out
 
+    def last_plan(self) -> Tuple[int, int]:
+        """(copy ranges of the first chunk — 0 when it was one copy outside the range branch —, pipeline
+        chunks) of the last host-buffer tokenize call."""
+        out = np.zeros(2, np.int32)
+        self._check(lib().pst_debug_fetch(self._h, 20, _ptr(out), out.nbytes))
+        return int(out[0]), int(out[1])
+
 
 class Decoder:
     """One libpst decoder context (one GPU): token ids → backbone atom37 coordinates."""
@@ -399,22 +408,32 @@ class Decoder:
         if rc != PST_OK:
             raise_for(rc, lib().pst_decoder_last_error(self._h).decode())
 
-    def decode(self, token_lists: Sequence[np.ndarray]) -> List[np.ndarray]:
-        """List of token-id arrays → list of atom37 position arrays [df·T, 37, 3] float32."""
+    def decode(self, token_lists: Sequence[np.ndarray], n_nodes: Optional[Sequence[int]] = None,
+               with_up_proj: bool = False):
+        """List of token-id arrays → list of atom37 position arrays [N_b, 37, 3] float32, N_b =
+        df·T_b, or `n_nodes[b]` (the graph's node count, df·T_b <= n < df·(T_b+1): the
+        autoencoder pass, pst_decoder_decode_ex). With `with_up_proj` also returns the per-protein
+        quantize_post_proj rows [T_b, 128]."""
         toks = [np.asarray(t, np.uint32).reshape(-1) for t in token_lists]
         off = np.zeros(len(toks) + 1, np.int64)
         off[1:] = np.cumsum([t.size for t in toks])
         flat = np.ascontiguousarray(np.concatenate(toks) if toks else np.zeros(0, np.uint32), np.uint32)
-        n_nodes = int(off[-1]) * self.df
-        out = np.zeros((max(n_nodes, 1), 37, 3), np.float32)
+        nin = None if n_nodes is None else np.ascontiguousarray(n_nodes, np.int32)
+        if nin is not None and nin.shape != (len(toks),):
+            raise ValueError(f"{nin.shape} node counts for {len(toks)} proteins")
+        n_total = int(off[-1]) * self.df if nin is None else int(nin.sum())
+        out = np.zeros((max(n_total, 1), 37, 3), np.float32)
         nn = np.zeros(len(toks), np.int32)
-        self._check(lib().pst_decoder_decode(self._h, _ptr(flat if flat.size else np.zeros(1, np.uint32)), _ptr(off),
-                                             len(toks), _ptr(out), _ptr(nn)))
+        up = np.zeros((max(int(off[-1]), 1), 128), np.float32) if with_up_proj else None
+        self._check(lib().pst_decoder_decode_ex(self._h, _ptr(flat if flat.size else np.zeros(1, np.uint32)), _ptr(off),
+                                                len(toks), _ptr(nin), _ptr(out), _ptr(nn), _ptr(up)))
         res, o = [], 0
         for n in nn:
             res.append(out[o:o + n].copy())
             o += int(n)
-        return res
+        if not with_up_proj:
+            return res
+        return res, [up[off[b]:off[b + 1]].copy() for b in range(len(toks))]
 
     def debug(self, which: int, n_floats: int) -> np.ndarray:
         out = np.zeros(n_floats, np.float32)

@@ -142,3 +142,71 @@ def overrides_for(codebook_size: int, df: int) -> List[str]:
     """The overrides `scripts/tokenize_pdb.py:109-113` builds."""
     return [f"model=gnn/ablation_{CODEBOOK_SURNAME[codebook_size]}_df_{df}.yaml",
             f"data=ablation_df_{df}.yaml"]
+
+
+_SURNAME_TO_CODEBOOK = {v: k for k, v in CODEBOOK_SURNAME.items()}
+# top-level keys of vq3d_inference.yaml that a Hydra override may set and that do not reach the
+# tokenize computation (the inference path draws no random numbers; mixed precision is off in
+# every shipped config and libpst computes in f32 regardless)
+_INERT_KEYS = {"random_seed", "mixed_precision", "deterministic", "use_remat", "zero_init"}
+
+
+def _override_file(group: str, value: str, pattern: str) -> Tuple[str, int]:
+    import re
+    m = re.fullmatch(pattern, value[:-5] if value.endswith(".yaml") else value)
+    if not m:
+        raise ValueError(f"unrecognised {group} override {group}={value!r}: the shipped configs are "
+                         + ("gnn/ablation_{0.5k,1.7k,4k,64k}_df_{1,2,4}.yaml" if group == "model"
+                            else "ablation_df_{1,2,4}.yaml"))
+    return m.group(1) if m.lastindex and m.lastindex > 1 else "", int(m.group(m.lastindex))
+
+
+def config_from_overrides(config_overrides: Optional[Sequence[str]] = None,
+                          weight_dir: Optional[str] = None) -> TokenizerConfig:
+    """The model the reference's `main(..., config_overrides=...)` composes
+    (`scripts/tokenize_pdb.py:40-45, 109-113`), without the YAML tree: (codebook, df) come from
+    `model=gnn/ablation_<K>_df_<df>.yaml` and `data=ablation_df_<df>.yaml`.
+
+    * `None` / `[]`: codebook 4096, df 1. (The reference's own defaults list names
+      `model: ablation_4k_df_1.yaml` / `data: ablation_1.yaml`, files that do not exist at those
+      paths, so its bare call fails in Hydra; 4k / df 1 is what those names intend.)
+    * only `model=…`: df from the model's name (its `max_out_len` = 512 / df).
+    * model and data naming different df: ValueError (the model's query PE table and the data's
+      token count disagree).
+    * `model.weight_paths=DIR` sets the weights directory; the inert top-level keys
+      (`random_seed`, `mixed_precision`, `deterministic`, `use_remat`, `zero_init`) are accepted.
+    * anything else (other groups, `ablation_continuous_*` models, malformed entries): ValueError
+      or, for continuous models, NotImplementedError — never a silent default.
+    """
+    cb: Optional[int] = None
+    df_model: Optional[int] = None
+    df_data: Optional[int] = None
+    for o in config_overrides or []:
+        if not isinstance(o, str) or "=" not in o:
+            raise ValueError(f"malformed config override {o!r} (expected key=value)")
+        k, v = o.split("=", 1)
+        k = k.strip().lstrip("+")
+        v = v.strip()
+        if k == "model":
+            if "continuous" in v:
+                raise NotImplementedError(f"{o}: continuous (codebook-free) models emit no tokens")
+            name, df_model = _override_file("model", v, r"gnn/ablation_(0\.5k|1\.7k|4k|64k)_df_(\d+)")
+            cb = _SURNAME_TO_CODEBOOK[name]
+        elif k == "data":
+            _, df_data = _override_file("data", v, r"ablation_df_(\d+)")
+        elif k == "model.weight_paths":
+            weight_dir = v
+        elif k in _INERT_KEYS:
+            continue
+        else:
+            raise ValueError(f"unrecognised config override {o!r}")
+    if df_model is not None and df_data is not None and df_model != df_data:
+        raise ValueError(f"model override is df {df_model} but data override is df {df_data}")
+    if cb is None and df_data not in (None, 1):
+        raise ValueError(f"data=ablation_df_{df_data}.yaml needs a matching model= override "
+                         "(the default model is ablation_4k_df_1)")
+    df = df_model if df_model is not None else (df_data or 1)
+    cfg = tokenizer_config(4096 if cb is None else cb, df)
+    if weight_dir:
+        cfg = dataclasses.replace(cfg, weight_dir=weight_dir)
+    return cfg

@@ -15,6 +15,8 @@ into libpst (`include/pst.h`):
   params_keys_conversion (:153-165)                     same (pst_amd.params)
   InferenceRunner.prepare_devices (:169-177)            HIP devices (backend "gpu" only)
   InferenceRunner.prepare_tokenize_fn (:179-191)        TokenizeFn: per-device libpst contexts
+  InferenceRunner.prepare_decode_fn / prepare_ae_fn /   DecodeFn / AutoEncodeFn / TokenToCodeFn
+    prepare_token_to_code_fn (:193-233)
   InferenceRunner.load_params (:236-248)                ReplicatedParams
   InferenceRunner.tokenize (:250-324)                   same loop, files and layout
 
@@ -167,7 +169,8 @@ class TokenizeFn:
     `devices[i]` (one host thread per device; the C calls release the GIL) and returns a dict
     with "tokens" uint32 [*batch_dims, seq_max_size // df] (padding rows carry the padded-token
     id exactly as the reference's output does) and "n_tokens" int32 [*batch_dims]
-    (= tokens_mask.sum(-1) of the reference graph). `random_key` is accepted and unused, as in
+    (= tokens_mask.sum(-1) of the reference graph) and "n_nodes" int32 [*batch_dims] (the graph's
+    n_node: residues with N, CA, C and O). `random_key` is accepted and unused, as in
     the reference's inference path (no stochastic op when is_training=False).
     """
 
@@ -204,17 +207,18 @@ class TokenizeFn:
             shard = batched_graph.shard(i)
             t = self._context(model_params, self.devices[i])
             pos, flags, off = _native.pack_samples(shard)
-            tok, nt, _ = t.tokenize_packed(pos, flags, off)
+            tok, nt, nn = t.tokenize_packed(pos, flags, off)
             rows = np.full((len(shard), out_len), pad, np.uint32)
             for b in range(len(shard)):
                 rows[b, :nt[b]] = tok[off[b]:off[b] + nt[b]]
             aux = self._aux(t, shard, off, nt, out_len) if self.emit_aux else None
-            return rows, nt, aux
+            return rows, nt, aux, nn
 
         res = list(self._pool.map(run, range(n_dev)))
         tokens = np.stack([r[0] for r in res]).reshape(*batched_graph.batch_dims, out_len)
         n_tokens = np.stack([r[1] for r in res]).reshape(*batched_graph.batch_dims)
-        out = {"tokens": tokens, "n_tokens": n_tokens}
+        n_nodes = np.stack([np.asarray(r[3], np.int32) for r in res]).reshape(*batched_graph.batch_dims)
+        out = {"tokens": tokens, "n_tokens": n_tokens, "n_nodes": n_nodes}
         if self.emit_aux:
             for key in res[0][2]:
                 if key == "histogram":
@@ -309,6 +313,13 @@ class InferenceRunner:
     @staticmethod
     def prepare_decode_fn(cfg: TokenizerConfig, devices: Sequence[int]) -> Callable:
         return DecodeFn(cfg, devices)
+
+    @staticmethod
+    def prepare_ae_fn(cfg: TokenizerConfig, devices: Sequence[int]) -> Callable:
+        """(`inference_runner.py:209-222`): the whole autoencoder pass, `AutoEncodeFn`."""
+        from .graph import set_graph_device
+        set_graph_device(list(devices)[0])
+        return AutoEncodeFn(cfg, devices)
 
     @staticmethod
     def prepare_token_to_code_fn(cfg: TokenizerConfig, devices: Sequence[int]) -> Callable:
@@ -493,6 +504,83 @@ class DecodeFn:
             d.close()
         self._ctx.clear()
         self._pool.shutdown(wait=True)
+
+
+class AutoEncodeFn:
+    """`prepare_ae_fn` (`inference_runner.py:209-222`): `Vq3D.__call__` (`model/model.py:194-259`)
+    — encode, quantize, decode and structure module in one call — for libpst.
+
+    `fn(model_params, random_key, batched_graph)` → `(decoded_structure, quantized_emb)`:
+      * quantized_emb: every `QuantizerOutput` field `prepare_tokenize_fn(emit_aux=True)` returns
+        (tokens, quantize, straight_through_quantized, continuous_embedding,
+        continuous_embedding_pre_proj, distances, soft_proba, perplexity) plus
+        `quantize_post_proj` [n_dev, bpd, seq_max/df, 128] = up_proj(quantize) (model.py:251;
+        padding rows, whose quantize is 0, hold the up_proj bias exactly as the reference's);
+      * decoded_structure: `final_atom_positions` [n_dev, bpd, seq_max, 37, 3] and
+        `final_atom_mask` [n_dev, bpd, seq_max, 37] int32 (folding.py:501-513).
+    The tokens are the tokenize path's (libpst encoder, bit-identical to `TokenizeFn`); the
+    decoder is libpst's (`pst_decoder_decode_ex`) on the graph's own node count, because
+    `__call__` decodes with the graph's `nodes_mask` (n_node residues) rather than df × the token
+    count the token-file decode uses. `__call__` passes the protein's real features to the
+    structure module, so atom37 positions come from `atom14_to_atom37` with the real `aatype`
+    and are masked by its `atom37_gt_exists` (preprocessing.py:285-306,
+    protein_structure_sample.py:93-118: the backbone N, CA, C, O of every kept residue): the four
+    backbone atoms of standard residues, zero for UNK residues (the UNK row of
+    RESTYPE_ATOM37_TO_ATOM14 / RESTYPE_ATOM37_MASK is all zero, all_atom.py:77-111), zero for
+    every other atom. The structure module's internal `representations` (unused by the
+    reference, folding.py:488-489) are not returned.
+    """
+
+    BACKBONE37 = (0, 1, 2, 4)  # N, CA, C, O
+
+    def __init__(self, cfg: TokenizerConfig, devices: Sequence[int]):
+        self.cfg = cfg
+        self.devices = list(devices)
+        self.tokenize = TokenizeFn(cfg, devices, emit_aux=True)
+        self.decode = DecodeFn(cfg, devices)
+
+    def __call__(self, model_params: ReplicatedParams, random_key: Any, batched_graph: ProteinBatch):
+        q = self.tokenize(model_params, random_key, batched_graph)
+        dims = batched_graph.batch_dims
+        n_dev = dims[0]
+        flat_tok = q["tokens"].reshape(n_dev, -1, q["tokens"].shape[-1])
+        flat_nt = q["n_tokens"].reshape(n_dev, -1)
+        flat_nn = q["n_nodes"].reshape(n_dev, -1)
+        bpd = flat_tok.shape[1]
+        L = self.cfg.seq_max_size
+        out_len = flat_tok.shape[-1]
+
+        def run(i):
+            dec = self.decode._context(model_params, self.devices[i])
+            return dec.decode([flat_tok[i, b, :flat_nt[i, b]] for b in range(bpd)],
+                              n_nodes=[int(n) for n in flat_nn[i]], with_up_proj=True)
+
+        res = list(self.decode._pool.map(run, range(n_dev)))
+        up_b = np.asarray(model_params.params["vq3_d/up_proj"]["b"], np.float32)
+        pos = np.zeros((n_dev, bpd, L, 37, 3), np.float32)
+        mask = np.zeros((n_dev, bpd, L, 37), np.int32)
+        post = np.broadcast_to(up_b, (n_dev, bpd, out_len, up_b.shape[0])).copy()
+        bb = list(self.BACKBONE37)
+        for i in range(n_dev):
+            atoms, ups = res[i]
+            for b in range(bpd):
+                s = batched_graph.samples[i * bpd + b]
+                kept = ~s.get_missing_backbone_coords_mask()
+                aa = np.argmax(np.asarray(s.aatype)[kept], axis=-1)
+                n = atoms[b].shape[0]
+                std = (aa[:n] < 20).astype(np.float32)  # restype_num: UNK rows map to zero
+                pos[i, b, :n, bb] = atoms[b][:, bb].transpose(1, 0, 2) * std[None, :, None]
+                mask[i, b, :n, bb] = 1
+                post[i, b, :ups[b].shape[0]] = ups[b]
+        structure = {"final_atom_positions": pos.reshape(*dims, L, 37, 3),
+                     "final_atom_mask": mask.reshape(*dims, L, 37)}
+        quantized_emb = {k: v for k, v in q.items() if k not in ("n_nodes",)}
+        quantized_emb["quantize_post_proj"] = post.reshape(*dims, out_len, up_b.shape[0])
+        return structure, quantized_emb
+
+    def close(self):
+        self.tokenize.close()
+        self.decode.close()
 
 
 def _normalised(histogram: np.ndarray) -> np.ndarray:

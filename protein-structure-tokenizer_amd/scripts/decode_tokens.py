@@ -17,13 +17,16 @@ from pst_amd.runner import InferenceRunner  # noqa: E402
 
 
 def main(sequences: List[str], structure_save_path: str, backend: str, batch_size_per_device: int = 8,
-         codebook_size: int = 4096, downsampling_ratio: int = 1, weights_dir: Optional[str] = None,
-         config_path: Optional[str] = None, config_overrides: Optional[List[str]] = None):
+         config_overrides: Optional[List[str]] = None, *, weights_dir: Optional[str] = None,
+         config_path: Optional[str] = None):
+    """The reference's `main` (`scripts/decode_tokens.py:32-80`), same positional signature; the
+    model comes from `config_overrides` as in `tokenize_pdb.main`
+    (`pst_amd.config.config_from_overrides`). Keyword-only extras: `weights_dir`, `config_path`."""
     if config_path:
         cfg = C.config_from_hydra(C.load_config("vq3d_inference", job_name="tokenize",
                                                 overrides=config_overrides, config_path=config_path))
     else:
-        cfg = C.tokenizer_config(codebook_size, downsampling_ratio)
+        cfg = C.config_from_overrides(config_overrides)
     runner = InferenceRunner()
     local_devices, n_local_device = runner.prepare_devices(backend=backend)
     decode_fn = runner.prepare_decode_fn(cfg=cfg, devices=local_devices)
@@ -55,9 +58,8 @@ def cli(argv=None):
         raise SystemExit(f"no model for codebook_size={args.codebook_size}, df={df}")
     tokens = [os.path.join(args.tokens_dir, f) for f in os.listdir(args.tokens_dir)]
     main(sequences=tokens, structure_save_path=args.structure_save_path, backend=args.backend,
-         batch_size_per_device=args.batch_size_per_device, codebook_size=args.codebook_size,
-         downsampling_ratio=df, weights_dir=args.weights_dir, config_path=args.config_path,
-         config_overrides=C.overrides_for(args.codebook_size, df))
+         batch_size_per_device=args.batch_size_per_device, weights_dir=args.weights_dir,
+         config_path=args.config_path, config_overrides=C.overrides_for(args.codebook_size, df))
 
 
 if __name__ == "__main__":

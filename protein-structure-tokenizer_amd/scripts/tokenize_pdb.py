@@ -7,16 +7,20 @@
 Same arguments and outputs (`OUT/<pdb stem>_tokens.npy`, uint32 [1, n_tokens]) as the
 reference (`scripts/tokenize_pdb.py:79-121`); `--backend` accepts only "gpu" (the default
 here). The model directory must hold `params.npz` (read with `allow_pickle=False`; the pickled
-`state_variables.npy` is not needed). Without `--config_path` the shipped hyper-parameters are
-used directly (`pst_amd.config.tokenizer_config`); with it, the reference's YAML tree is
-composed the same way the reference does (`config_overrides` from the two flags).
+`state_variables.npy` is not needed). The CLI builds the reference's two overrides from its
+flags (`model=gnn/ablation_<K>_df_<df>.yaml`, `data=ablation_df_<df>.yaml`) and `main` selects
+the model from them (`pst_amd.config.config_from_overrides`, no YAML tree needed); with
+`--config_path` the reference's YAML tree is composed from the same overrides instead.
+The reference's CLI defaults `--backend` to "cpu" (an XLA target); libpst has no CPU path, so
+the default here is "gpu" and any other backend raises NotImplementedError.
 
 One process drives every local GPU (a host thread per GPU, like the reference's pmap). Under
 `torchrun` (WORLD_SIZE > 1) each rank instead takes GPU LOCAL_RANK (modulo the visible devices)
 and an LPT shard of the PDB list balanced on file size (`runner.shard_for_rank`); there is no
 collective on the data path. Rank 0 creates `--token_save_path` exactly as the reference does
-(`inference_runner.py:265`, FileExistsError if it exists) and broadcasts the outcome over a gloo
-group before any rank starts; each rank writes through a private `.rank<N>` directory inside it.
+(`inference_runner.py:265`, FileExistsError if it exists; any other OSError is re-raised on
+every rank with its type) and broadcasts the outcome over a gloo group before any rank starts;
+each rank writes through a private `.rank<N>` directory inside it.
 """
 import argparse
 import os
@@ -32,13 +36,24 @@ from pst_amd.runner import InferenceRunner, shard_for_rank  # noqa: E402
 
 
 def main(pdbs: List[str], token_save_path: str, backend: str, batch_size_per_device: int = 8,
-         codebook_size: int = 4096, downsampling_ratio: int = 1, weights_dir: Optional[str] = None,
-         config_path: Optional[str] = None, config_overrides: Optional[List[str]] = None):
+         config_name: Optional[str] = None, config_overrides: Optional[List[str]] = None, *,
+         weights_dir: Optional[str] = None, config_path: Optional[str] = None):
+    """The reference's `main` (`scripts/tokenize_pdb.py:32-73`), same positional signature.
+
+    The model is selected by `config_overrides` exactly as the reference composes it
+    (`model=gnn/ablation_<K>_df_<df>.yaml`, `data=ablation_df_<df>.yaml`,
+    `pst_amd.config.config_from_overrides`); an unrecognised override raises instead of
+    falling back to a default. `config_name` is accepted and, as in the reference, not used
+    (the composed config is always `vq3d_inference`) unless `config_path` points at the
+    reference's YAML tree, which is then composed with Hydra's rules under that name.
+    Keyword-only extras: `weights_dir` (directory of `params.npz`; default the config's
+    `weight_paths`) and `config_path`.
+    """
     if config_path:
-        cfg = C.config_from_hydra(C.load_config("vq3d_inference", job_name="tokenize",
+        cfg = C.config_from_hydra(C.load_config(config_name or "vq3d_inference", job_name="tokenize",
                                                 overrides=config_overrides, config_path=config_path))
     else:
-        cfg = C.tokenizer_config(codebook_size, downsampling_ratio)
+        cfg = C.config_from_overrides(config_overrides)
     runner = InferenceRunner()
     local_devices, n_local_device = runner.prepare_devices(backend=backend)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,13 +89,23 @@ def _create_output_on_rank0(token_save_path: str, rank: int) -> None:
     try:
         msg = [None]
         if rank == 0:
+            # any failure (exists, permission, bad parent...) must reach every rank before the
+            # broadcast, or the other ranks would wait in it until the gloo timeout
             try:
                 os.makedirs(token_save_path, exist_ok=False)
-            except FileExistsError as e:
-                msg = [str(e)]
+            except OSError as e:
+                msg = [(type(e).__name__, e.errno, e.strerror, e.filename)]
+            except Exception as e:  # noqa: BLE001 — e.g. a TypeError from a bad path object
+                msg = [("RuntimeError", None, f"{type(e).__name__}: {e}", None)]
         dist.broadcast_object_list(msg, src=0)
         if msg[0] is not None:
-            raise FileExistsError(msg[0])
+            name, errno_, strerror, filename = msg[0]
+            if name == "RuntimeError":
+                raise RuntimeError(strerror)
+            exc = {"FileExistsError": FileExistsError, "PermissionError": PermissionError,
+                   "FileNotFoundError": FileNotFoundError, "NotADirectoryError": NotADirectoryError
+                   }.get(name, OSError)
+            raise exc(errno_, strerror, filename)
     finally:
         if own:
             dist.destroy_process_group()
@@ -114,9 +139,8 @@ def cli(argv=None):
         raise SystemExit(f"no model for codebook_size={args.codebook_size}, df={df}")
     pdbs = [os.path.join(args.pdb_dir, f) for f in os.listdir(args.pdb_dir)]
     main(pdbs=pdbs, token_save_path=args.token_save_path, backend=args.backend,
-         batch_size_per_device=args.batch_size_per_device, codebook_size=args.codebook_size,
-         downsampling_ratio=df, weights_dir=args.weights_dir, config_path=args.config_path,
-         config_overrides=C.overrides_for(args.codebook_size, df))
+         batch_size_per_device=args.batch_size_per_device, weights_dir=args.weights_dir,
+         config_path=args.config_path, config_overrides=C.overrides_for(args.codebook_size, df))
 
 
 if __name__ == "__main__":

@@ -27,7 +27,7 @@ def run(rank, world, port, pdb_dir, model_dir, out_dir, result_q):
     pdbs_sorted = sorted(pdbs)
     mine = runner.shard_for_rank(pdbs_sorted, rank, world, weights=[os.path.getsize(p) for p in pdbs_sorted])
     cli.main(pdbs=pdbs, token_save_path=out_dir, backend="gpu", batch_size_per_device=2,
-             codebook_size=4096, downsampling_ratio=1, weights_dir=model_dir)
+             config_overrides=["model=gnn/ablation_4k_df_1.yaml", "data=ablation_df_1.yaml"], weights_dir=model_dir)
     # host-side gather of what each rank handled (test bookkeeping only, not the data path)
     got = [None] * world
     dist.all_gather_object(got, sorted(os.path.basename(p) for p in mine))
@@ -70,7 +70,7 @@ def run_existing_dir(rank, world, port, pdb_dir, model_dir, out_dir, result_q):
     pdbs = [os.path.join(pdb_dir, f) for f in os.listdir(pdb_dir)]
     try:
         cli.main(pdbs=pdbs, token_save_path=out_dir, backend="gpu", batch_size_per_device=2,
-                 codebook_size=4096, downsampling_ratio=1, weights_dir=model_dir)
+                 config_overrides=["model=gnn/ablation_4k_df_1.yaml", "data=ablation_df_1.yaml"], weights_dir=model_dir)
         result_q.put((rank, "no error"))
     except FileExistsError:
         result_q.put((rank, "FileExistsError"))

@@ -36,14 +36,17 @@ def test_chunked_h2d_is_bitwise_identical(cb, df):
     R = int(off[-1])
     outs = []
     # one copy and one graph launch (the reference point), then the first chunk copied in 4 / 8
-    # protein ranges with the graph per range, at 1, 3 and 8 chunks
-    for chunks, ranges in ((1, 1), (1, None), (1, 8), (3, None), (8, None)):
+    # protein ranges with the graph per range, at 1, 3 and 8 chunks. The batch (~350 tasks) is
+    # below the default policy's half-round gate, so the default (None) takes one copy and an
+    # explicit PST_H2D_GRAPH_RANGES forces the range branch; the plan each call took is checked.
+    for chunks, ranges, want_ranges in ((1, 1, 0), (1, None, 0), (1, 4, 4), (1, 8, 8), (3, 4, 4), (8, 8, 8)):
         t = _ctx(chunks, cb, df, ranges)
         tok, nt, nn = t.tokenize_packed(pos, flags, off)
+        assert t.last_plan() == (want_ranges, chunks), (chunks, ranges)
         tok2, _, _ = t.tokenize_packed(pos, flags, off)  # a second call on the same context
         aux = t.aux(R)
         T = int(nt.sum())
-        ca = t.codebook_aux(T, distances=True, soft_proba=False)
+        ca = t.codebook_aux(T, distances=True, soft_proba=cb == 4096)  # 64 000: ~0.7 GB per copy
         outs.append((tok, nt, nn, aux, ca))
         assert np.array_equal(tok, tok2)
         t.close()
@@ -56,6 +59,8 @@ def test_chunked_h2d_is_bitwise_identical(cb, df):
         assert np.array_equal(o[4]["argmin"], base[4]["argmin"])
         assert np.array_equal(o[4]["histogram"], base[4]["histogram"])
         assert np.array_equal(o[4]["distances"].view(np.uint32), base[4]["distances"].view(np.uint32))
+        if cb == 4096:
+            assert np.array_equal(o[4]["soft_proba"].view(np.uint32), base[4]["soft_proba"].view(np.uint32))
 
 
 def test_default_pipeline_policy_matches_one_shot():
@@ -68,7 +73,9 @@ def test_default_pipeline_policy_matches_one_shot():
     os.environ.pop("PST_H2D_CHUNKS", None)
     t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
     tok, nt, nn = t.tokenize_packed(pos, flags, off)
+    plan = t.last_plan()
     t.close()
+    assert plan == (4, 2)  # default policy: 1 + 3 rounds, first chunk in 4 copy ranges
     t1 = _ctx(1)
     tok1, nt1, nn1 = t1.tokenize_packed(pos, flags, off)
     t1.close()
@@ -120,10 +127,12 @@ def test_two_proteins_small_first():
     samples = [synthetic.synthetic_protein(60, 41), synthetic.synthetic_protein(480, 42)]
     pos, flags, off = pack_samples(samples)
     outs = []
-    for ranges in (1, None):
+    # 4 ranges requested on 2 proteins: the cut keeps one range, inside the range branch
+    for ranges, plan in ((1, (0, 1)), (4, (1, 1))):
         t = _ctx(1, ranges=ranges)
         for _ in range(3):
             outs.append(t.tokenize_packed(pos, flags, off))
+            assert t.last_plan() == plan
         t.close()
     os.environ.pop("PST_H2D_CHUNKS")
     for o in outs[1:]:

@@ -147,7 +147,9 @@ class _OracleCtx:
 
     def tokenize_packed(self, pos, flags, off):
         tok, nt = O.tokenize_batch(self.blob, self.levels, self.df, pos, flags, off, n_threads=4)
-        return tok, nt, nt * self.df
+        full = np.all(flags[:, [0, 1, 2, 4]] & 1, axis=1)  # N, CA, C, O present
+        nn = np.array([int(full[off[b]:off[b + 1]].sum()) for b in range(len(off) - 1)], np.int32)
+        return tok, nt, nn
 
     def close(self):
         pass
