@@ -194,7 +194,7 @@ def plan_only(args, rank, world):
         dist.destroy_process_group()
 
 
-def reference_exact_match(args, ids, tok, off):
+def reference_exact_match(args, ids, tok, off, plan=None):
     """Token ids of the fixture proteins this rank holds vs the reference's float64 forward
     (forward_ref_wide.npz: bench256_p0..7 at 4096/df 1, bench512_p0..1 at 64000/df 4), with the
     rounding-margin report (tests/golden/refwide.py)."""
@@ -224,7 +224,13 @@ def reference_exact_match(args, ids, tok, off):
     if not reps:
         return None
     r = refwide.merge(reps)
-    return {"proteins": prots, "tokens_compared": r["tokens"], "identical": r["identical"], "rate": r["rate"],
+    cuts = plan["cuts"] if plan else None
+    chunk_of = {}
+    if cuts:
+        pos_of = {p: i for i, p in enumerate(ids)}
+        chunk_of = {p: int(np.searchsorted(cuts, pos_of[p], side="right") - 1) for p in prots}
+    return {"proteins": prots, "pipeline_chunk_of_protein": chunk_of,
+            "tokens_compared": r["tokens"], "identical": r["identical"], "rate": r["rate"],
             "identical_to_f64_reference": int(sum(x["identical_to_f64_reference"] for x in reps)),
             "min_margin": r["min_margin"], "margin_histogram_all": r["margin_histogram_all"],
             "margin_histogram_mismatches": r["margin_histogram_mismatches"],
@@ -274,7 +280,7 @@ def casp14_end_to_end(tk):
     return res
 
 
-def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok):
+def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=None):
     """(reference-as-computed torch CPU at all allowed cores and at 8 threads, ragged C port, and
     the GPU-vs-C-oracle exact match on the port's sample)."""
     import torch
@@ -302,17 +308,37 @@ def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok):
                                   "over all K), PyTorch-CPU float32 (oracle/reference_as_computed.py) + the C "
                                   f"graph; torch.set_num_threads({threads}) of {cores} cores available"}
     torch.set_num_threads(cores)
-    m = min(args.port_sample, len(samples))
-    log(f"C-port CPU baseline, {cores} threads, {m} proteins")
-    sub_R = int(off[m])
+    # the C-port sample is spread over the whole workload (every stride-th protein), so it checks
+    # every pipeline chunk the timed step runs, not only the first
+    nb = len(samples)
+    stride = max(1, -(-nb // max(1, args.port_sample)))
+    sel = np.arange(0, nb, stride)
+    lens = off[sel + 1] - off[sel]
+    soff = np.concatenate(([0], np.cumsum(lens))).astype(np.int64)
+    rows = np.concatenate([np.arange(off[i], off[i + 1]) for i in sel])
+    sub_R = int(soff[-1])
+    log(f"C-port CPU baseline, {cores} threads, {len(sel)} proteins (every {stride}th)")
     t1 = time.perf_counter()
-    otok, _ = O.tokenize_batch(blob, levels, args.df, pos[:sub_R], flags[:sub_R], off[:m + 1], n_threads=cores)
+    otok, _ = O.tokenize_batch(blob, levels, args.df, pos[rows], flags[rows], soff, n_threads=cores)
     cpu_s = time.perf_counter() - t1
     port = {"value": round(sub_R / cpu_s, 1), "unit": "residues/s", "cores": cores, "kind": "port",
-            "sample": f"first {m} proteins ({sub_R} residues), oracle/pst_oracle.c (ragged, real residues only, "
-                      f"the GPU's canonical op order), OpenMP over proteins, {cpu_s:.1f} s"}
-    match = int(np.sum(gpu_tok[:sub_R] == otok[:sub_R]))
+            "sample": f"{len(sel)} proteins (every {stride}th of the workload, {sub_R} residues), oracle/pst_oracle.c "
+                      f"(ragged, real residues only, the GPU's canonical op order), OpenMP over proteins, {cpu_s:.1f} s"}
+    gsel = gpu_tok[rows]
+    by_chunk = []
+    cuts = plan["cuts"] if plan else [0, nb]
+    scheds = plan["schedules"] if plan else [None]
+    for c in range(len(cuts) - 1):
+        in_c = (sel >= cuts[c]) & (sel < cuts[c + 1])
+        r_c = np.concatenate([np.arange(soff[j], soff[j + 1]) for j in np.nonzero(in_c)[0]]) if in_c.any() \
+            else np.zeros(0, np.int64)
+        by_chunk.append({"proteins": [int(cuts[c]), int(cuts[c + 1])], "schedule": scheds[c],
+                         "proteins_compared": int(in_c.sum()), "tokens_compared": int(len(r_c)),
+                         "identical": int(np.sum(gsel[r_c] == otok[r_c]))})
+    match = int(np.sum(gsel == otok))
     exact = {"tokens_compared": sub_R, "identical": match, "rate": match / sub_R,
+             "proteins_compared": int(len(sel)), "sample": f"every {stride}th protein",
+             "by_pipeline_chunk": by_chunk,
              "against": "C oracle (bitwise canonical path)"}
     return out[cores], out.get(8), port, exact
 
@@ -380,6 +406,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    plan = tk.last_plan_detail()  # chunks and layer schedule of the timed step (rank 0's share)
     log(f"rank {rank}: {args.steps} timed steps in {elapsed:.2f} s")
     stats = torch.tensor(times + [elapsed], dtype=torch.float64, device=red_dev)
     total_res = torch.tensor([R], dtype=torch.float64, device=red_dev)
@@ -408,7 +435,7 @@ def main():
                    "note": "rank 0's shard, median of 5 after one warm-up"}
 
     # exact match vs the reference fixtures of the proteins this rank holds (summed over ranks)
-    ref_match = reference_exact_match(args, ids, tok, off)
+    ref_match = reference_exact_match(args, ids, tok, off, plan)
     if world > 1:
         cnt = torch.tensor([ref_match["tokens_compared"], ref_match["identical"]] if ref_match else [0, 0],
                            dtype=torch.float64, device=red_dev)
@@ -482,7 +509,7 @@ def main():
     cpu = cpu8 = port = exact = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baselines")
-        cpu, cpu8, port, exact = cpu_baselines(args, samples, blob, levels, pos, flags, off, tok)
+        cpu, cpu8, port, exact = cpu_baselines(args, samples, blob, levels, pos, flags, off, tok, plan)
 
     if rank == 0:
         mode = "weak" if args.weak else "strong"
@@ -511,6 +538,7 @@ def main():
                                 "pst_tokenize_f32, float32 positions as the PDB path holds them")
                              + "), median over steps of the max over ranks"),
             "other_input_format": other_input,
+            "pipeline_plan": plan,
             "ms_per_step_mean_bracketed": round(elapsed / args.steps * 1e3, 3),
             "elapsed_s": round(elapsed, 3),
             "device_resident": {"residues_per_s_per_gpu": round(R / float(np.median(dts)), 1),

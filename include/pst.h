@@ -259,8 +259,10 @@ void* pst_stream(pst_ctx* ctx);
 /* Debug: copy an intermediate of the LAST call to host.
  *   which = 0..3: node features after init embed / MPNN layer 1..3, [R,128] (raw slot rows)
  *   which = 10:   edge features [R*k, 32] float (27 used), which = 11: senders [R*k] int32
- *   which = 20:   int32[2] plan of the last pst_tokenize(_f32) call: {copy ranges of its first
- *                 chunk (0 = one copy, the range branch not taken), pipeline chunks} */
+ *   which = 20:   int32[20] plan of the last pst_tokenize(_f32) call: [0] copy ranges of its first
+ *                 chunk (0 = one copy, the range branch not taken), [1] pipeline chunks C,
+ *                 [2 .. 2+C] the chunks' first proteins (and n_prot), [11 .. 11+C-1] each chunk's
+ *                 layer schedule (0 fused one wave per task, 1 fused two waves per task, 2 split) */
 int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes);
 
 #ifdef __cplusplus

@@ -254,7 +254,11 @@ struct pst_ctx {
   hipEvent_t range_ev[8] = {};  // one per copy range of the first chunk (GraphRanges)
   hipEvent_t idle_ev = nullptr; // recorded on `stream` before copy_stream overwrites the inputs
   bool chunked_last = false; // last call was pipelined: per-layer debug intermediates hold its last chunk only
-  int32_t last_plan[2] = {0, 0}; // last host call: copy ranges of its first chunk (0 = one copy), chunks (pst_debug_fetch 20)
+  // last host call's plan (pst_debug_fetch 20): [0] copy ranges of its first chunk (0 = one copy),
+  // [1] chunks, [2..10] protein cuts of the chunks, [11..18] each chunk's layer schedule
+  // (0 fused one wave per task, 1 fused two waves per task, 2 split)
+  int32_t last_plan[20] = {};
+  int32_t last_sched = 0;  // schedule of the last run()
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
   // optional per-stage timing (HIP events on ctx->stream)
   bool timing = false;
@@ -598,6 +602,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
       split && n_tasks <= (ctx->node_coop >= 0 ? ctx->node_coop : (int64_t)(NODE_COOP_SIMD_FRACTION * ctx->n_simds));
   env_threshold(ctx->half_tasks, "PST_HALF_TASKS");
   const bool half = !split && (ctx->half_tasks >= 0 ? ctx->half_tasks != 0 : use_half_tasks(n_tasks, ctx->n_simds));
+  ctx->last_sched = split ? 2 : half ? 1 : 0;
   float* msg_rows = nullptr;
   int32_t bpw = 1;
   if (split) {
@@ -1007,18 +1012,22 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
       HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->copy_ev[k], 0));
     }
     if (k == 0) {
+      std::fill(std::begin(ctx->last_plan), std::end(ctx->last_plan), 0);
       ctx->last_plan[0] = nr > 1 ? gr.n : 0;  // 0: one copy, no range branch
       ctx->last_plan[1] = n_chunks;
+      for (int q = 0; q <= n_chunks; ++q) ctx->last_plan[2 + q] = cut[q];
     }
     if (n_chunks == 1) {
       rc = run(ctx, pos64(0), w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes, false, 0, pos32(0),
                gr.n > 0 ? &gr : nullptr);
       if (rc) return rc;
+      ctx->last_plan[11] = ctx->last_sched;
       break;
     }
     rc = run(ctx, pos64(r0), w.flags + 37 * r0, loc.data(), b1 - b0, w.tokens + r0, w.n_tok + b0, w.n_nodes + b0,
              false, r0, pos32(r0), gr.n > 0 ? &gr : nullptr);
     if (rc) return rc;
+    ctx->last_plan[11 + k] = ctx->last_sched;
   }
   if (n_chunks > 1) {
     // the batch as a whole for pst_aux / pst_codebook_aux: offsets, token tiles and last_* of all
@@ -1238,7 +1247,7 @@ int pst_codebook_aux(pst_ctx* ctx, float* distances, float* soft_proba, uint32_t
 
 int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes) {
   if (!ctx || ctx->last_R == 0) return PST_E_INVALID;
-  if (which == 20) {  // the last host call's plan: {copy ranges of its first chunk, chunks}
+  if (which == 20) {  // the last host call's plan (see pst_ctx::last_plan)
     if (bytes < sizeof(ctx->last_plan)) return fail(ctx, PST_E_INVALID, "debug buffer too small");
     std::memcpy(out, ctx->last_plan, sizeof(ctx->last_plan));
     return PST_OK;

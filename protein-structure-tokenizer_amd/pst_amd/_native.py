@@ -364,9 +364,18 @@ class Tokenizer:
     def last_plan(self) -> Tuple[int, int]:
         """(copy ranges of the first chunk — 0 when it was one copy outside the range branch —, pipeline
         chunks) of the last host-buffer tokenize call."""
-        out = np.zeros(2, np.int32)
+        p = self.last_plan_detail()
+        return p["ranges"], p["chunks"]
+
+    def last_plan_detail(self) -> dict:
+        """The last host-buffer tokenize call's plan: copy ranges, chunks, the chunks' protein cuts
+        and each chunk's layer schedule ("fused", "fused_half" = two waves per task, "split")."""
+        out = np.zeros(20, np.int32)
         self._check(lib().pst_debug_fetch(self._h, 20, _ptr(out), out.nbytes))
-        return int(out[0]), int(out[1])
+        C = int(out[1])
+        names = {0: "fused", 1: "fused_half", 2: "split"}
+        return {"ranges": int(out[0]), "chunks": C, "cuts": [int(x) for x in out[2:3 + C]],
+                "schedules": [names[int(x)] for x in out[11:11 + C]]}
 
 
 class Decoder:

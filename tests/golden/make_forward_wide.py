@@ -22,6 +22,7 @@ token ids, its FSQ-bounded latents `bounded` (float64) and the per-token roundin
 
     python tests/golden/make_forward_wide.py [--jobs 8] [--only PREFIX]        # float64 (the fixture)
     python tests/golden/make_forward_wide.py --pe32                             # + JAX-f32 PE argument
+    python tests/golden/make_forward_wide.py --f32                              # + the all-float32 rendering
 """
 import argparse
 import hashlib
@@ -51,7 +52,8 @@ def case_list():
         nm = str(nm)
         cases.append((f"casp_{nm}_k4096_df1", ("casp", nm), 4096, 1))
         cases.append((f"casp_{nm}_k64000_df1", ("casp", nm), 64000, 1))
-    for p in range(8):
+    # the first 8 proteins of the bench (its first pipeline chunk) and 4 from the later chunks
+    for p in list(range(8)) + [200, 511, 777, 1023]:
         cases.append((f"bench256_p{p}_k4096_df1", ("syn", 256, 1000 + p), 4096, 1))
     for p in range(2):
         cases.append((f"bench512_p{p}_k64000_df4", ("syn", 512, 1000 + p), 64000, 4))
@@ -146,9 +148,20 @@ def run_case(case, f64=True, pe32=False):
     n = int(g.n_node[0])
     T = n // df
     b = np.asarray(res["continuous_embedding"][0, :T], dtype=np.float64)
+    # the FSQ input z = down_proj(pre_proj) (model.py:417-419), evaluated from the run's own
+    # pre-projection embedding with the same weights (Linear: x @ w + b)
+    pre = np.asarray(res["continuous_embedding_pre_proj"][0, :T], dtype=ft)
+    dp = params["vq3_d/down_proj"]
+    z = (pre @ dp["w"].astype(ft) + dp["b"].astype(ft)).astype(np.float64)
+    if not f64:  # the whole reference forward in float32 (the shim with f64=False: JAX's x64-off dtypes)
+        out = {"tokens_f32": np.asarray(res["tokens"][0, :T]).astype(np.uint32), "bounded_f32": b,
+               "margin_f32": margins(b), "z_f32": z}
+        if cb == 4096:
+            out["pre_proj_f32"] = np.asarray(res["continuous_embedding_pre_proj"][0, :T], dtype=np.float32)
+        return name, out
     if pe32:
         out = {"tokens_pe32": np.asarray(res["tokens"][0, :T]).astype(np.uint32), "bounded_pe32": b,
-               "margin_pe32": margins(b)}
+               "margin_pe32": margins(b), "z_pe32": z}
         if cb == 4096:
             out["pre_proj_pe32"] = np.asarray(res["continuous_embedding_pre_proj"][0, :T], dtype=np.float32)
         return name, out
@@ -156,7 +169,7 @@ def run_case(case, f64=True, pe32=False):
         "in_positions": pos32, "in_flags": flags,
         "meta": np.array([n, T, cb, df, D, PARAM_SEED], np.int64),
         "tokens": np.asarray(res["tokens"][0, :T]).astype(np.uint32),
-        "bounded": b, "margin": margins(b),
+        "bounded": b, "margin": margins(b), "z": z,
     }
     if sha is not None:
         out["input_sha256"] = np.array(sha)
@@ -170,6 +183,10 @@ def run_case_pe32(case):
     return run_case(case, pe32=True)
 
 
+def run_case_f32(case):
+    return run_case(case, f64=False)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=8)
@@ -177,6 +194,9 @@ def main():
     ap.add_argument("--pe32", action="store_true",
                     help="add the variant whose PE argument is float32 as under JAX (tokens_pe32, "
                          "bounded_pe32, margin_pe32, pre_proj_pe32); see jax_f32_pe_argument")
+    ap.add_argument("--f32", action="store_true",
+                    help="add the rendering with the whole reference forward in float32 (tokens_f32, "
+                         "bounded_f32, margin_f32, z_f32, pre_proj_f32)")
     args = ap.parse_args()
     sys.path.insert(0, HERE)
     import _refenv
@@ -193,9 +213,14 @@ def main():
             if str(old[key]) != sha:
                 sys.exit(f"{name}: synthetic generator no longer reproduces the stored inputs")
     with get_context("spawn").Pool(args.jobs) as pool:
-        for name, res in pool.imap_unordered(run_case_pe32 if args.pe32 else run_case, cases):
+        fn = run_case_pe32 if args.pe32 else run_case_f32 if args.f32 else run_case
+        for name, res in pool.imap_unordered(fn, cases):
             for k, v in res.items():
                 old[f"{name}/{k}"] = v
+            if args.f32:
+                flips = int(np.sum(res["tokens_f32"] != old[f"{name}/tokens"]))
+                print(f"{name}: f32 tokens differing from the all-f64 run = {flips}", flush=True)
+                continue
             if args.pe32:
                 flips = int(np.sum(res["tokens_pe32"] != old[f"{name}/tokens"]))
                 print(f"{name}: pe32 tokens differing from the all-f64 run = {flips}", flush=True)

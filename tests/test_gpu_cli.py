@@ -223,4 +223,6 @@ def test_prepare_ae_fn_equals_tokenize_then_decode():
         for b, m in enumerate(lens):
             got = st["final_atom_positions"][0, b, :m]
             want = d["final_atom_positions"][0, b, :m]
-            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (cb, df, b)
+            bb = [0, 1, 2, 4]  # backbone atoms bitwise; the others are zeros (signs may differ)
+            assert np.array_equal(got[:, bb].view(np.uint32), want[:, bb].view(np.uint32)), (cb, df, b)
+            assert np.array_equal(got, want), (cb, df, b)
