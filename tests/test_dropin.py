@@ -127,3 +127,32 @@ def test_main_unknown_override_raises_before_any_work(tmp_path, oracle_runner):
     with pytest.raises(ValueError):
         tokenize_pdb.main([], str(out), "gpu", config_overrides=["model=gnn/ablation_2k_df_1.yaml"])
     assert not out.exists() and "cfg" not in oracle_runner
+
+
+AE_GOLD = os.path.join(ROOT, "tests", "golden", "ae_ref.npz")
+
+
+@pytest.mark.skipif(not os.path.exists(AE_GOLD), reason="ae_ref.npz not generated")
+def test_ae_fixture_tokens_equal_oracle_and_layout():
+    """The reference's autoencoder pass (`make_ae_golden.py`): its tokens equal the C oracle's on
+    the same inputs and weights, the node count is not a multiple of df where the case says so,
+    the atom mask is the backbone of the kept residues, and the UNK residue's atoms are zero."""
+    from oracle import oracle as O
+    F = np.load(AE_GOLD)
+    for c in sorted({k.split("/")[0] for k in F.files}):
+        n, n_node, T, cb, df, D, pseed = (int(v) for v in F[c + "/meta"])
+        pos = F[c + "/in_positions"].astype(np.float64)
+        fl = F[c + "/in_flags"]
+        blob = P.pack(P.params_keys_conversion(P.random_full_params(D, pseed)), D)
+        got = O.tokenize(blob, C.LEVELS[cb], df, pos, fl)
+        assert got["graph"]["n"] == n_node and len(got["tokens"]) == T
+        assert np.array_equal(got["tokens"], F[c + "/tokens"]), c
+        mask = F[c + "/final_atom_mask"]
+        assert mask.shape == (512, 37) and mask[:n_node][:, [0, 1, 2, 4]].all() and mask.sum() == 4 * n_node
+        aa = F[c + "/in_aatype"]
+        kept = np.all(fl[:, [0, 1, 2, 4]] & 1, axis=1)
+        unk = np.nonzero(aa[kept] == 20)[0]
+        atoms = F[c + "/final_atom_positions"]
+        assert len(unk) == 1 and np.all(atoms[unk] == 0) and np.all(atoms[:, [3] + list(range(5, 37))] == 0)
+        if df > 1:
+            assert n_node % df != 0

@@ -14,17 +14,24 @@ from pst_amd._native import pack_samples
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _clear_pipeline_env():
+    yield
+    for k in ("PST_H2D_CHUNKS", "PST_H2D_GRAPH_RANGES"):
+        os.environ.pop(k, None)
+
+
 def _ctx(chunks, cb=4096, df=1, ranges=None):
-    """ranges: copy ranges of the first chunk (PST_H2D_GRAPH_RANGES; None = the default 4)."""
+    """ranges: copy ranges of the first chunk (PST_H2D_GRAPH_RANGES; None = the policy). The
+    context reads both variables at its FIRST tokenize call, so they stay set until the test
+    ends (or the next _ctx call replaces them)."""
     from pst_amd._native import Tokenizer
-    os.environ["PST_H2D_CHUNKS"] = str(chunks)  # read at the context's first call
+    os.environ["PST_H2D_CHUNKS"] = str(chunks)
     if ranges is None:
         os.environ.pop("PST_H2D_GRAPH_RANGES", None)
     else:
         os.environ["PST_H2D_GRAPH_RANGES"] = str(ranges)
-    t = Tokenizer(0, cb, df, P.random_blob(6, 1234))
-    os.environ.pop("PST_H2D_GRAPH_RANGES", None)
-    return t
+    return Tokenizer(0, cb, df, P.random_blob(6, 1234))
 
 
 @pytest.mark.parametrize("cb,df", [(4096, 1), (64000, 4)])
@@ -39,10 +46,19 @@ def test_chunked_h2d_is_bitwise_identical(cb, df):
     # protein ranges with the graph per range, at 1, 3 and 8 chunks. The batch (~350 tasks) is
     # below the default policy's half-round gate, so the default (None) takes one copy and an
     # explicit PST_H2D_GRAPH_RANGES forces the range branch; the plan each call took is checked.
-    for chunks, ranges, want_ranges in ((1, 1, 0), (1, None, 0), (1, 4, 4), (1, 8, 8), (3, 4, 4), (8, 8, 8)):
+    # (the first chunk of a forced 3- or 8-chunk plan holds only a few proteins, so it gets at
+    # most that many ranges)
+    for chunks, ranges, want_ranges in ((1, 1, 0), (1, None, 0), (1, 4, 4), (1, 8, 8), (3, 4, None), (8, 8, None)):
         t = _ctx(chunks, cb, df, ranges)
         tok, nt, nn = t.tokenize_packed(pos, flags, off)
-        assert t.last_plan() == (want_ranges, chunks), (chunks, ranges)
+        plan = t.last_plan_detail()
+        assert plan["chunks"] == chunks and len(plan["cuts"]) == chunks + 1, (chunks, ranges, plan)
+        if want_ranges is None and plan["cuts"][1] == 1:  # one protein: one copy
+            assert plan["ranges"] == 0, (chunks, ranges, plan)
+        elif want_ranges is None:
+            assert 1 <= plan["ranges"] <= min(ranges, plan["cuts"][1]), (chunks, ranges, plan)
+        else:
+            assert plan["ranges"] == want_ranges, (chunks, ranges, plan)
         tok2, _, _ = t.tokenize_packed(pos, flags, off)  # a second call on the same context
         aux = t.aux(R)
         T = int(nt.sum())
