@@ -590,6 +590,19 @@ __global__ void k_ipa_points(const float* __restrict__ qpl /*[N][144]*/, const f
 // Invariant point attention for query residue i (folding.py:69-289): logits over all N residues,
 // softmax, then the 2112 output features [scalar 192 | local points x,y,z 3×96 | norms 96 |
 // pair 1536]. One workgroup per i.
+// The attention weights live in LDS transposed, attT[j][ATT_LD] (heads 0..11 of key j, row
+// stride 13 words: odd, so a wave's 64 consecutive keys of one head hit 32 distinct banks in the
+// softmax, and the MFMA operand reads below conflict at most 2-way).
+// MFMA_PAIR: the pair attention Σ_j att[h][j]·z_ij[c] (12 heads × 128 channels, the largest of
+// the weighted sums) runs on v_mfma_f32_16x16x4_f32 — D[c][h] = Σ_j z[j][c]·att[h][j], wave w
+// owning channels 32w..32w+31 as two 16-row blocks, the 12 heads in columns 0..11 of the 16.
+// That instruction is a k-ascending fmaf chain (tools/probe/mfma_probe.hip: 256/256 bitwise), so
+// every sum is the same in-order chain over j from 0 as the VALU form (!MFMA_PAIR, kept for the
+// A/B test): identical bits. The value sums (480 outputs, one head each) stay on the VALU.
+constexpr int ATT_LD = 13;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool MFMA_PAIR>
 __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /*[N][192]*/,
                                                   const float* __restrict__ kvs_all /*[N][384]*/,
                                                   const float* __restrict__ qpg, const float* __restrict__ kvpg_all,
@@ -601,7 +614,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
                                                   const float* __restrict__ kT_all /*[192][Ntot]*/,
                                                   const float* __restrict__ kpT_all /*[144][Ntot]*/, int Ntot,
                                                   int ld /*row stride of qs and kvs*/) {
-  __shared__ float att[12][512];
+  __shared__ float attT[512 * ATT_LD];
   __shared__ float res_pt[12 * 8 * 3];
   const int64_t ig = blockIdx.x;
   const int tid = threadIdx.x;
@@ -650,7 +663,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
         const float d2 = (dx * dx + dy * dy) + dz * dz;
         pt += pw[h] * d2;
       }
-      att[h][j] = (sc + (-0.5f * pt)) + bb[h];
+      attT[j * ATT_LD + h] = (sc + (-0.5f * pt)) + bb[h];
     }
   }
   __syncthreads();
@@ -659,23 +672,66 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
     const int lane = tid & 63, w = tid >> 6;
     for (int h = w; h < 12; h += 4) {
       float mx = -INFINITY;
-      for (int j = lane; j < N; j += 64) mx = fmaxf(mx, att[h][j]);
+      for (int j = lane; j < N; j += 64) mx = fmaxf(mx, attT[j * ATT_LD + h]);
       for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
       float s = 0.0f;
       for (int j = lane; j < N; j += 64) {
-        float e = expf(att[h][j] - mx);
-        att[h][j] = e;
+        float e = expf(attT[j * ATT_LD + h] - mx);
+        attT[j * ATT_LD + h] = e;
         s += e;
       }
       for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-      for (int j = lane; j < N; j += 64) att[h][j] = att[h][j] / s;
+      for (int j = lane; j < N; j += 64) attT[j * ATT_LD + h] = attT[j * ATT_LD + h] / s;
     }
   }
   __syncthreads();
   float* f = feat + ig * 2112;
-  // One pass over the keys feeds all 2016 weighted sums of this query: per thread the pair
-  // attention of channel c for heads hg, hg+2, ... (6 sums) and value outputs o = tid and
-  // tid + 256 (scalar values 0..191, global value points 192..479). Each sum is its own in-order
+  if (MFMA_PAIR) {
+    // pair attention on the matrix cores: lane (i = lane & 15, g = lane >> 4) feeds A = z[4s+g][c0+i]
+    // and B = att[head i][4s+g] (0 for the 4 padding heads); after the chain it holds
+    // D[c0 + 4g + r][head i], r = 0..3
+    const int lane = tid & 63, w = tid >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int cA = 32 * w + i, cB = cA + 16;
+    const bool hv = i < 12;
+    f32x4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
+    const float* zrow = zln + (int64_t)g * 128;
+    int s = 0;
+    const int S = N / 4;  // whole k-steps; a tail of N % 4 keys runs as one zero-padded step
+    for (; s + 4 <= S; s += 4) {
+      float za[4], zb[4], bt4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* zr = zrow + (int64_t)(4 * (s + u)) * 128;
+        za[u] = zr[cA];
+        zb[u] = zr[cB];
+        bt4[u] = hv ? attT[(4 * (s + u) + g) * ATT_LD + i] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        accA = __builtin_amdgcn_mfma_f32_16x16x4f32(za[u], bt4[u], accA, 0, 0, 0);
+        accB = __builtin_amdgcn_mfma_f32_16x16x4f32(zb[u], bt4[u], accB, 0, 0, 0);
+      }
+    }
+    for (; 4 * s < N; ++s) {
+      // last steps (and a partial one): keys j >= N enter as 0·0 products, which leave the chain unchanged
+      const int j = 4 * s + g;
+      const bool jv = j < N;
+      const float* zr = zrow + (int64_t)(4 * s) * 128;
+      const float za = jv ? zr[cA] : 0.0f, zb = jv ? zr[cB] : 0.0f;
+      const float bv = hv && jv ? attT[j * ATT_LD + i] : 0.0f;
+      accA = __builtin_amdgcn_mfma_f32_16x16x4f32(za, bv, accA, 0, 0, 0);
+      accB = __builtin_amdgcn_mfma_f32_16x16x4f32(zb, bv, accB, 0, 0, 0);
+    }
+    if (hv) {
+      float* o = f + 576 + i * 128 + 32 * w + 4 * g;
+      *reinterpret_cast<float4*>(o) = make_float4(accA[0], accA[1], accA[2], accA[3]);
+      *reinterpret_cast<float4*>(o + 16) = make_float4(accB[0], accB[1], accB[2], accB[3]);
+    }
+  }
+  // Value sums (and, without MFMA_PAIR, the pair attention): per thread the value outputs
+  // o = tid and tid + 256 (scalar values 0..191, global value points 192..479) and, VALU form, the
+  // pair attention of channel c for heads hg, hg+2, ... (6 sums). Each sum is its own in-order
   // fmaf chain over j; loads run 8 keys ahead.
   {
     const int c = tid & 127, hg = tid >> 7;
@@ -706,27 +762,33 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
       float zv[8], v0[8], v1[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        zv[u] = zr[(int64_t)(j + u) * 128];
+        if (!MFMA_PAIR) zv[u] = zr[(int64_t)(j + u) * 128];
         v0[u] = vsrc[0][(int64_t)(j + u) * vstride[0]];
         v1[u] = vok[1] ? vsrc[1][(int64_t)(j + u) * vstride[1]] : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
+        if (!MFMA_PAIR) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) pacc[k] = __builtin_fmaf(att[hg + 2 * k][j + u], zv[u], pacc[k]);
-        vacc[0] = __builtin_fmaf(att[vh[0]][j + u], v0[u], vacc[0]);
-        vacc[1] = __builtin_fmaf(att[vh[1]][j + u], v1[u], vacc[1]);
+          for (int k = 0; k < 6; ++k) pacc[k] = __builtin_fmaf(attT[(j + u) * ATT_LD + hg + 2 * k], zv[u], pacc[k]);
+        }
+        vacc[0] = __builtin_fmaf(attT[(j + u) * ATT_LD + vh[0]], v0[u], vacc[0]);
+        vacc[1] = __builtin_fmaf(attT[(j + u) * ATT_LD + vh[1]], v1[u], vacc[1]);
       }
     }
     for (; j < N; ++j) {
-      const float zv = zr[(int64_t)j * 128];
+      if (!MFMA_PAIR) {
+        const float zv = zr[(int64_t)j * 128];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) pacc[k] = __builtin_fmaf(att[hg + 2 * k][j], zv, pacc[k]);
-      vacc[0] = __builtin_fmaf(att[vh[0]][j], vsrc[0][(int64_t)j * vstride[0]], vacc[0]);
-      if (vok[1]) vacc[1] = __builtin_fmaf(att[vh[1]][j], vsrc[1][(int64_t)j * vstride[1]], vacc[1]);
+        for (int k = 0; k < 6; ++k) pacc[k] = __builtin_fmaf(attT[j * ATT_LD + hg + 2 * k], zv, pacc[k]);
+      }
+      vacc[0] = __builtin_fmaf(attT[j * ATT_LD + vh[0]], vsrc[0][(int64_t)j * vstride[0]], vacc[0]);
+      if (vok[1]) vacc[1] = __builtin_fmaf(attT[j * ATT_LD + vh[1]], vsrc[1][(int64_t)j * vstride[1]], vacc[1]);
     }
+    if (!MFMA_PAIR) {
 #pragma unroll
-    for (int u = 0; u < 6; ++u) f[576 + (hg + 2 * u) * 128 + c] = pacc[u];
+      for (int u = 0; u < 6; ++u) f[576 + (hg + 2 * u) * 128 + c] = pacc[u];
+    }
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int o = tid + 256 * m;
@@ -1156,6 +1218,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   gemm(st, S.ln_a, 128, W.left, S.left, 256, Ni, 0);
   gemm(st, S.ln_a, 128, W.right, S.right, 256, Ni, 0);
   const bool fused = !getenv("PST_DECODE_UNFUSED");
+  const bool ipa_mfma = !getenv("PST_DECODE_IPA_VALU");  // A/B: the VALU pair sum (same bits)
   if (fused) {
     layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
     gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
@@ -1199,8 +1262,8 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     gemm_raw(st, S.act, 384, dec->d_ipa_w, 384, 1152, dec->d_ipa_b, S.ipa_in, 1152, Ni, 0);
     hipLaunchKernelGGL(k_ipa_points, dim3((unsigned)N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg,
                        S.kvs, S.kT, S.kpT, Ni, 1152);
-    hipLaunchKernelGGL(k_ipa_attn, dim3((unsigned)N), dim3(256), 0, st, S.qs, S.kvs, S.qpg, S.kvpg, S.b2d, S.zln,
-                       dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152);
+    hipLaunchKernelGGL(ipa_mfma ? k_ipa_attn<true> : k_ipa_attn<false>, dim3((unsigned)N), dim3(256), 0, st, S.qs,
+                       S.kvs, S.qpg, S.kvpg, S.b2d, S.zln, dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152);
     gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
     layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
     gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);

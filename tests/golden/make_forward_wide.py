@@ -9,6 +9,14 @@ float64 — the same recipe as `make_golden.py forward` — on:
 * `syn56_missing9`: 56 residues, 9 without backbone → 47 kept, the reference's short-protein
   branch (preprocessing.py:229-260), at df 1 and df 2.
 
+Three renderings of the same forward: float64 throughout (the fixture's `tokens`, `bounded`,
+`z`, `pre_proj`); `_pe32`, float64 with the PE argument rounded to float32 as JAX forms it with
+x64 off (`jax_f32_pe_argument`, the reference's own PE values); `_f32`, the shim in float32 mode
+(float32 weights and edge features) with the PE in JAX's float32 dtypes (`jax_f32_pe_values`).
+The `_f32` rendering is mixed precision, not XLA's float32: NumPy promotes integer-array × float
+products (the FSQ levels, masks built with default-dtype ones) to float64 where JAX x64-off keeps
+float32, and NumPy's tanh / reductions are not XLA's. `dtypes_f32` records the output dtypes.
+
 Inputs are never regenerated silently: CASP14 inputs come from `casp14_atom37.npz`, the short
 case from `graph_golden.npz`, and synthetic inputs are regenerated and checked against the
 SHA-256 stored in the fixture (`tests/test_fixture_recipes.py` repeats that check on CPU), so the
@@ -107,6 +115,28 @@ def jax_f32_pe_argument(pel):
     pel.PositionalEncodingLayer.sinusoidal_positional_encoding = pe
 
 
+def jax_f32_pe_values(pel):
+    """For the float32 rendering (--f32): the sinusoidal PE exactly as `jax_f32_pe_argument` forms
+    its argument, with cos / sin evaluated in float32 (correctly rounded) and a float32 result —
+    JAX's dtypes with x64 off. (The shim's plain float32 mode would evaluate `x * math.pi` on
+    NumPy integer arrays in float64.)"""
+    import math
+
+    def pe(self, x, n, d, k):
+        x = np.asarray(x)
+        k = np.asarray(k)
+        odd = np.mod(k, 2).astype(np.float32)
+        num = np.where(np.mod(k, 2) == 1, 2 * (k - 1), 2 * k).astype(np.float32)
+        e = num / np.float32(d)
+        pw = np.power(np.float64(n), e.astype(np.float64)).astype(np.float32)
+        arg = (x.astype(np.float32) * np.float32(math.pi)) / pw
+        cs = np.cos(arg.astype(np.float64)).astype(np.float32)
+        sn = np.sin(arg.astype(np.float64)).astype(np.float32)
+        return odd * cs - (odd - np.float32(1)) * sn
+
+    pel.PositionalEncodingLayer.sinusoidal_positional_encoding = pe
+
+
 def run_case(case, f64=True, pe32=False):
     os.environ["OMP_NUM_THREADS"] = "1"
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
@@ -116,6 +146,9 @@ def run_case(case, f64=True, pe32=False):
     if pe32:
         from structure_tokenizer.model import positional_encoding_layer
         jax_f32_pe_argument(positional_encoding_layer)
+    if not f64:
+        from structure_tokenizer.model import positional_encoding_layer
+        jax_f32_pe_values(positional_encoding_layer)
     import jax
     import haiku as hk
     from structure_tokenizer.data import preprocessing as ref_pp
@@ -153,9 +186,11 @@ def run_case(case, f64=True, pe32=False):
     pre = np.asarray(res["continuous_embedding_pre_proj"][0, :T], dtype=ft)
     dp = params["vq3_d/down_proj"]
     z = (pre @ dp["w"].astype(ft) + dp["b"].astype(ft)).astype(np.float64)
-    if not f64:  # the whole reference forward in float32 (the shim with f64=False: JAX's x64-off dtypes)
+    if not f64:  # the reference forward with float32 weights, inputs and PE (see the module docstring)
         out = {"tokens_f32": np.asarray(res["tokens"][0, :T]).astype(np.uint32), "bounded_f32": b,
-               "margin_f32": margins(b), "z_f32": z}
+               "margin_f32": margins(b), "z_f32": z,
+               "dtypes_f32": np.array([str(np.asarray(res["continuous_embedding_pre_proj"]).dtype),
+                                       str(np.asarray(res["continuous_embedding"]).dtype)])}
         if cb == 4096:
             out["pre_proj_f32"] = np.asarray(res["continuous_embedding_pre_proj"][0, :T], dtype=np.float32)
         return name, out

@@ -211,3 +211,24 @@ def test_gemm_mfma_matches_valu_gemm(monkeypatch):
     for a, b in zip(base, other):
         assert np.all(np.isfinite(a)) and np.all(np.isfinite(b))
         assert np.max(np.abs(a - b)) < 1e-3
+
+
+def test_ipa_pair_sum_mfma_matches_valu_bitwise(monkeypatch):
+    """k_ipa_attn's pair attention Σ_j att[h][j]·z_ij on v_mfma_f32_16x16x4_f32 (default) vs the
+    VALU fmaf chains (PST_DECODE_IPA_VALU=1): the instruction is a k-ascending fmaf chain, so both
+    are the same in-order chain over j — identical bits, ragged group with key counts that are not
+    multiples of 4 (the zero-padded last k-step), df 1 and df 4."""
+    from pst_amd._native import Decoder
+    rng = np.random.default_rng(23)
+    for cb, df, lens in ((4096, 1, (64, 23, 130, 7)), (64000, 4, (9, 31, 128))):
+        D = len(LEVELS[cb])
+        toks = [rng.integers(0, cb, n) for n in lens]
+        dec = Decoder(0, cb, df, P.pack_decoder(P.random_full_params(D, 29), D))
+        base = dec.decode(toks)
+        monkeypatch.setenv("PST_DECODE_IPA_VALU", "1")
+        other = dec.decode(toks)
+        monkeypatch.delenv("PST_DECODE_IPA_VALU")
+        dec.close()
+        for a, b in zip(base, other):
+            assert np.all(np.isfinite(a))
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
