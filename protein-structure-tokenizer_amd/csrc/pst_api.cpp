@@ -245,6 +245,8 @@ struct pst_ctx {
   // pst_tokenize's H2D pipeline: proteins copied in chunks on copy_stream, chunk k+1's copy
   // overlapping chunk k's compute on `stream` (H2D_MAX_CHUNKS events)
   hipStream_t copy_stream = nullptr;
+  hipStream_t copy_stream2 = nullptr;  // odd graph ranges of the first chunk (PST_H2D_COPY_STREAMS=2)
+  int64_t h2d_streams = -2;            // PST_H2D_COPY_STREAMS: copy streams for the graph ranges (1 or 2)
   hipEvent_t copy_ev[8] = {};
   int64_t h2d_chunks = -2;  // PST_H2D_CHUNKS: force the chunk count (1 = no pipeline); -1 = policy
   int64_t h2d_first = -2;   // PST_H2D_FIRST_ROUNDS: rounds in the first pipelined chunk; -1 = H2D_FIRST_ROUNDS
@@ -843,10 +845,11 @@ int pst_destroy(pst_ctx* ctx) {
   if (ctx->msg) (void)hipFree(ctx->msg);
   for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_U, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
-  if (ctx->copy_stream) {
-    (void)hipStreamSynchronize(ctx->copy_stream);
-    (void)hipStreamDestroy(ctx->copy_stream);
-  }
+  for (hipStream_t cs : {ctx->copy_stream, ctx->copy_stream2})
+    if (cs) {
+      (void)hipStreamSynchronize(cs);
+      (void)hipStreamDestroy(cs);
+    }
   for (hipEvent_t e : ctx->copy_ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->range_ev)
@@ -962,6 +965,7 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
                                                                          : H2D_GRAPH_RANGES);
   if (!ctx->copy_stream) {
     HIPCHK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->copy_stream2, hipStreamNonBlocking));
     for (int k = 0; k < H2D_MAX_CHUNKS; ++k) HIPCHK(hipEventCreateWithFlags(&ctx->copy_ev[k], hipEventDisableTiming));
     for (int k = 0; k < 8; ++k) HIPCHK(hipEventCreateWithFlags(&ctx->range_ev[k], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->idle_ev, hipEventDisableTiming));
@@ -969,11 +973,13 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
   // inputs are overwritten on copy_stream only after everything queued on `stream` so far
   HIPCHK(hipEventRecord(ctx->idle_ev, ctx->stream));
   HIPCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->idle_ev, 0));
-  auto copy_rows = [&](int64_t r0, int64_t r1) -> int {
+  env_threshold(ctx->h2d_streams, "PST_H2D_COPY_STREAMS");
+  const bool two_streams = ctx->h2d_streams == 2;
+  if (two_streams) HIPCHK(hipStreamWaitEvent(ctx->copy_stream2, ctx->idle_ev, 0));
+  auto copy_rows = [&](int64_t r0, int64_t r1, hipStream_t cs) -> int {
     HIPCHK(hipMemcpyAsync(d_pos_bytes + es * 111 * r0, h_pos_bytes + es * 111 * r0, es * 111 * (r1 - r0),
-                          hipMemcpyHostToDevice, ctx->copy_stream));
-    HIPCHK(hipMemcpyAsync(w.flags + 37 * r0, atom_flags + 37 * r0, 37 * (r1 - r0), hipMemcpyHostToDevice,
-                          ctx->copy_stream));
+                          hipMemcpyHostToDevice, cs));
+    HIPCHK(hipMemcpyAsync(w.flags + 37 * r0, atom_flags + 37 * r0, 37 * (r1 - r0), hipMemcpyHostToDevice, cs));
     return PST_OK;
   };
   // chunk k: copied on copy_stream, its compute queued on `stream` behind the copy's event(s); the
@@ -1001,12 +1007,13 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
       gr.n = (int)rcut.size() - 1;
       gr.cut = rcut.data();
       for (int q = 0; q < gr.n; ++q) {
-        rc = copy_rows(r0 + loc[rcut[q]], r0 + loc[rcut[q + 1]]);
+        hipStream_t cs = two_streams && (q & 1) ? ctx->copy_stream2 : ctx->copy_stream;
+        rc = copy_rows(r0 + loc[rcut[q]], r0 + loc[rcut[q + 1]], cs);
         if (rc) return rc;
-        HIPCHK(hipEventRecord(ctx->range_ev[q], ctx->copy_stream));
+        HIPCHK(hipEventRecord(ctx->range_ev[q], cs));
       }
     } else {
-      rc = copy_rows(r0, r1);
+      rc = copy_rows(r0, r1, ctx->copy_stream);
       if (rc) return rc;
       HIPCHK(hipEventRecord(ctx->copy_ev[k], ctx->copy_stream));
       HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->copy_ev[k], 0));

@@ -22,13 +22,14 @@ def test_wide_synthetic_inputs_reproduce():
         assert M.input_sha(pos, fl) == str(F[c + "/input_sha256"]), c
         assert np.array_equal(pos, F[c + "/in_positions"]) and np.array_equal(fl, F[c + "/in_flags"])
         checked += 1
-    assert checked == 10
+    assert checked == 14  # bench256 p0-7, p200, p511, p777, p1023; bench512 p0-1
 
 
 def test_bench_workload_is_the_fixture_workload():
-    """bench.py's proteins 0..7 (seed 1000 + p, 256 residues) are the fixture's bench256 cases."""
-    b = synthetic.synthetic_batch(2, 256, seed=1000)
-    for p, s in enumerate(b):
+    """bench.py's proteins p (seed 1000 + p, 256 residues) are the fixture's bench256 cases, in its
+    first pipeline chunk (0, 1) and in the later ones (200, 511, 777, 1023)."""
+    for p in (0, 1, 200, 511, 777, 1023):
+        s = synthetic.synthetic_protein(256, 1000 + p)
         assert np.array_equal(s.atom37_positions.astype(np.float32), F[f"bench256_p{p}_k4096_df1/in_positions"])
 
 
