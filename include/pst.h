@@ -262,7 +262,9 @@ void* pst_stream(pst_ctx* ctx);
  *   which = 20:   int32[20] plan of the last pst_tokenize(_f32) call: [0] copy ranges of its first
  *                 chunk (0 = one copy, the range branch not taken), [1] pipeline chunks C,
  *                 [2 .. 2+C] the chunks' first proteins (and n_prot), [11 .. 11+C-1] each chunk's
- *                 layer schedule (0 fused one wave per task, 1 fused two waves per task, 2 split) */
+ *                 layer schedule (0 fused one wave per task, 1 fused two waves per task, 2 split),
+ *                 [19] the last chunk's downsampler form (0 one wave per tile, 1 four waves per
+ *                 tile, 2 two waves per tile) */
 int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes);
 
 #ifdef __cplusplus

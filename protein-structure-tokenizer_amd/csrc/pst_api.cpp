@@ -240,6 +240,8 @@ struct pst_ctx {
   int64_t edge_waves = -2;   // PST_EDGE_WAVES: split-schedule edge waves target; -1 = SPLIT_EDGE_WAVES
   int64_t node_coop = -2;    // PST_NODE_COOP: k_mpnn_node_coop iff split and n_tasks <= this; -1 = default
   int64_t down_coop = -2;    // PST_DOWN_COOP: k_down_coop iff n_tiles <= this; -1 = default; -2 = not read yet
+  int64_t down_pair = -2;    // PST_DOWN_PAIR: 1 = k_down_pair whenever not coop (df 1), 0 = never; -1 = one round of tiles
+  int32_t last_down_form = 0;  // pst::DOWN_* of the last run (pst_debug_fetch 20, plan[19])
   int64_t half_tasks = -2;   // PST_HALF_TASKS: 1 = fused layers always two waves per task, 0 = never; -1 = policy
   std::vector<int64_t> h_offsets;
   // pst_tokenize's H2D pipeline: proteins copied in chunks on copy_stream, chunk k+1's copy
@@ -258,7 +260,8 @@ struct pst_ctx {
   bool chunked_last = false; // last call was pipelined: per-layer debug intermediates hold its last chunk only
   // last host call's plan (pst_debug_fetch 20): [0] copy ranges of its first chunk (0 = one copy),
   // [1] chunks, [2..10] protein cuts of the chunks, [11..18] each chunk's layer schedule
-  // (0 fused one wave per task, 1 fused two waves per task, 2 split)
+  // (0 fused one wave per task, 1 fused two waves per task, 2 split), [19] the last chunk's
+  // downsampler form (pst::DOWN_*)
   int32_t last_plan[20] = {};
   int32_t last_sched = 0;  // schedule of the last run()
   float* dbg[3] = {nullptr, nullptr, nullptr};  // PST_DEBUG=1: node features after each layer
@@ -684,6 +687,12 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   env_threshold(ctx->down_coop, "PST_DOWN_COOP");
   const int64_t coop_max = ctx->down_coop >= 0 ? ctx->down_coop : (int64_t)(DOWN_COOP_SIMD_FRACTION * ctx->n_simds);
   const bool down_coop = ctx->df == 1 && (int64_t)n_tiles <= coop_max;
+  // above the coop threshold but at most one round of tiles, k_down_pair puts the two tracks of
+  // a tile on two waves (k_down<1> would leave every SIMD's second wave slot empty)
+  env_threshold(ctx->down_pair, "PST_DOWN_PAIR");
+  const bool down_pair = ctx->df == 1 && !down_coop &&
+                         (ctx->down_pair >= 0 ? ctx->down_pair != 0 : (int64_t)n_tiles <= ctx->n_simds);
+  ctx->last_down_form = down_coop ? pst::DOWN_COOP : down_pair ? pst::DOWN_PAIR : pst::DOWN_ONE_WAVE;
   if (!down_coop) HIPCHK(hipMemcpyAsync(w.h1, hbuf[3], sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
   pst::DownArgs d{};
   d.n_tiles = n_tiles;
@@ -720,7 +729,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   d.bounded_out = w.bounded + 8 * out_row0;
   d.quant_out = w.quant + 8 * out_row0;
   d.pre_proj_out = w.pre_proj + 128 * out_row0;
-  if (d.n_tiles > 0) pst::launch_down(ctx->df, d, down_coop, st);
+  if (d.n_tiles > 0) pst::launch_down(ctx->df, d, ctx->last_down_form, st);
   mark(ctx, 6);
   HIPCHK(hipGetLastError());
   ctx->last_R = R;
@@ -1029,12 +1038,14 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
                gr.n > 0 ? &gr : nullptr);
       if (rc) return rc;
       ctx->last_plan[11] = ctx->last_sched;
+      ctx->last_plan[19] = ctx->last_down_form;
       break;
     }
     rc = run(ctx, pos64(r0), w.flags + 37 * r0, loc.data(), b1 - b0, w.tokens + r0, w.n_tok + b0, w.n_nodes + b0,
              false, r0, pos32(r0), gr.n > 0 ? &gr : nullptr);
     if (rc) return rc;
     ctx->last_plan[11 + k] = ctx->last_sched;
+    ctx->last_plan[19] = ctx->last_down_form;
   }
   if (n_chunks > 1) {
     // the batch as a whole for pst_aux / pst_codebook_aux: offsets, token tiles and last_* of all

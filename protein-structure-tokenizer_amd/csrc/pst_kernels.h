@@ -155,7 +155,10 @@ void launch_knn(const KnnArgs& a, hipStream_t st);
 // node_coop (split schedule only): node update as k_mpnn_node_coop, four waves per 32 receivers
 void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st);
 // coop (df 1 only): one workgroup per tile, the GEMMs split over its four waves (small batches)
-void launch_down(int df, const DownArgs& a, bool coop, hipStream_t st);
+// downsampler forms (df 1; df 2/4 always run k_down<df>): one wave per tile (k_down<1>), four
+// waves per tile (k_down_coop), two waves per tile, one track each (k_down_pair). Identical bits.
+enum { DOWN_ONE_WAVE = 0, DOWN_COOP = 1, DOWN_PAIR = 2 };
+void launch_down(int df, const DownArgs& a, int form, hipStream_t st);
 void launch_fsq_aux(const FsqAuxArgs& a, int n_prot, hipStream_t st);
 // Y = (init or 0) + X·W (+ b): init / b perm-ordered 128-vectors (either may be null)
 void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, const float* init, float* Y,

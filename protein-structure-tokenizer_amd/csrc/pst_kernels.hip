@@ -1142,6 +1142,173 @@ __global__ __launch_bounds__(256, DF == 1 ? 2 : 1) void k_down(DownArgs a) {
   }
 }
 
+// ------------------------------------------------------------------- k_down_pair
+// k_down<1> with the two tracks of a tile on two waves, for batches of at most one round of tiles
+// (the N = 8 share of config 3: 1 024 tiles, where k_down<1> leaves every SIMD's second wave slot
+// empty). Per block b, the original-track wave ("o") computes v_b = LN(o_b)·Wv, hands it over
+// through LDS (double buffered, one workgroup barrier per block) and then runs the original
+// transition o_{b+1} = o_b + T(LN(o_b)); the resampled-track wave ("r") computes the gate from
+// LN(r), waits for v_b, and runs gating, output projection and the resampled transition. The r
+// wave's chain per block is 384 k-steps instead of 704. Every value is computed by the same
+// operations in the same order as in k_down<1> — only which wave runs them changes — so the bits
+// are identical (test_down_coop_and_one_wave_identical forces all three forms). Workgroup = 4
+// waves = 2 tiles (waves 2i, 2i+1 = tile i's r and o waves); every wave passes the same three
+// barriers, tiles past the end included.
+__global__ __launch_bounds__(256, 2) void k_down_pair(DownArgs a) {
+  __shared__ float vx[2][2][64 * 64];  // [tile in workgroup][buffer][register][lane]
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tw = w >> 1, role_o = w & 1;
+  const int tile_id = blockIdx.x * 2 + tw;
+  const bool live = tile_id < a.n_tiles;
+  int b = 0, t0 = 0, T = 0;
+  int64_t base = 0;
+  if (live) {
+    b = a.tile_prot[tile_id];
+    t0 = a.tile_t0[tile_id];
+    base = a.offsets[b];
+    T = a.n_nodes[b];
+  }
+  const int t = t0 + (lane & 31);
+  const bool valid = live && t < T;
+  const int tc = valid ? t : (T > 0 ? T - 1 : 0);
+  if (!role_o) {
+    // ---- the resampled-track wave
+    float* rrow = a.r_buf + (base + tc) * 128;
+    if (live) {
+      Tile r;
+      tile_load_perm(r, a.RPE + (int64_t)tc * 128);
+      if (valid) tile_store_perm(r, rrow);
+    }
+    for (int blk = 0; blk < 3; ++blk) {
+      const DownBlockW& W = a.blk[blk];
+      const float* xs = vx[tw][blk & 1];
+      Tile wa;
+      if (live) {  // gating logits LN_q(r) Wg + bg; after the handover, v · sigmoid(logits)
+        Tile q;
+        tile_load_perm(q, rrow);
+        tile_layer_norm(q, W.qn_s, W.qn_o);
+        tile_zero(wa);
+        tile_gemm(wa, q, W.wg);
+        tile_add_vec(wa, W.gb);
+      }
+      __syncthreads();
+      if (!live) continue;
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) wa.m[M][r] = xs[(M * 16 + r) * 64 + lane] * c_sigmoid(wa.m[M][r]);
+      Tile o;
+      tile_zero(o);
+      tile_gemm(o, wa, W.wo);
+      tile_add_vec(o, W.ob);
+      Tile r;
+      tile_load_perm(r, rrow);
+      tile_add(r, o);
+      if (valid) tile_store_perm(r, rrow);
+      Tile x = r;
+      tile_layer_norm(x, W.rt_ln_s, W.rt_ln_o);
+      Tile acc;
+      tile_zero(acc);
+      for (int ck = 0; ck < 2; ++ck) {
+        Tile hid;
+        tile_zero(hid);
+        tile_gemm(hid, x, W.rt_w1 + ck * 64 * 64);
+        tile_gemm_f(acc, hid, W.rt_w2 + ck * 64 * 64, ActBiasRelu{W.rt_b1 + ck * 128});
+      }
+      tile_add_vec(acc, W.rt_b2);
+      tile_load_perm(r, rrow);
+      tile_add(r, acc);
+      if (valid) tile_store_perm(r, rrow);
+    }
+    if (!live) return;
+    // spherical norm, down_proj, FSQ (as k_down<1>)
+    Tile r;
+    tile_load_perm(r, rrow);
+    float s = 0.0f;
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s = s + r.m[M][q] * r.m[M][q];
+    float nrm = sqrtf(s + __shfl_xor(s, 32, 64)) + 1e-6f;
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) r.m[M][q] = r.m[M][q] / nrm;
+    f32x16 z;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = 0.0f;
+    tile_gemm_narrow(z, r, a.down_w);
+    uint32_t part_idx = 0;
+    const int h = lane >> 5;
+    const int64_t orow_i = base + t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int d = q + 4 * h;
+      if (d < a.D) {
+        float zz = z[q] + a.down_b[d];
+        float bnd = c_tanh(zz + a.fsq_shift[d]) * a.fsq_half[d] - a.fsq_off[d];
+        float qv = rintf(bnd);
+        part_idx += (uint32_t)((int)qv + a.fsq_L[d] / 2) * (uint32_t)a.fsq_basis[d];
+        if (valid) {
+          a.bounded_out[orow_i * 8 + d] = bnd;
+          a.quant_out[orow_i * 8 + d] = qv;
+        }
+      }
+    }
+    uint32_t idx = part_idx + (uint32_t)__shfl_xor((int)part_idx, 32, 64);
+    if (valid) {
+      if (h == 0) a.tokens_out[orow_i] = idx;
+      float4* pp = reinterpret_cast<float4*>(a.pre_proj_out + orow_i * 128);
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pp[(32 * M + 8 * q + 4 * h) / 4] =
+              make_float4(r.m[M][4 * q], r.m[M][4 * q + 1], r.m[M][4 * q + 2], r.m[M][4 * q + 3]);
+    }
+    return;
+  }
+  // ---- the original-track wave: v_b for the r wave, then the original transition
+  float* orow = a.o_buf + (base + tc) * 128;
+  for (int blk = 0; blk < 3; ++blk) {
+    const DownBlockW& W = a.blk[blk];
+    float* xs = vx[tw][blk & 1];
+    if (live) {  // v_b = LN(o_b)·Wv (+0.0f: fmaf(1, v, 0), as k_down<1>)
+      Tile x;
+      tile_load_perm(x, orow);
+      tile_layer_norm(x, W.dn_s, W.dn_o);
+      Tile wa;
+      tile_zero(wa);
+      tile_gemm(wa, x, W.wv);
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xs[(M * 16 + r) * 64 + lane] = wa.m[M][r] + 0.0f;
+    }
+    __syncthreads();
+    if (live && blk < 2) {  // original transition (block 3's is dead)
+      Tile x;
+      tile_load_perm(x, orow);
+      tile_layer_norm(x, W.ot_ln_s, W.ot_ln_o);
+      Tile acc;
+      tile_zero(acc);
+      for (int ck = 0; ck < 2; ++ck) {
+        Tile hid;
+        tile_zero(hid);
+        tile_gemm(hid, x, W.ot_w1 + ck * 64 * 64);
+        tile_add_vec(hid, W.ot_b1 + ck * 128);
+        tile_relu(hid);
+        tile_gemm(acc, hid, W.ot_w2 + ck * 64 * 64);
+      }
+      tile_add_vec(acc, W.ot_b2);
+      tile_load_perm(x, orow);
+      tile_add(x, acc);
+      if (valid) tile_store_perm(x, orow);
+    }
+  }
+}
+
 // ------------------------------------------------------------------- k_down_coop
 // Small-batch form of k_down<1>: one workgroup per 32-token tile, wave w computes output
 // block w (channels 32w … 32w+31) of every GEMM, so a tile's 20 sequential 128x128 GEMMs take
@@ -1622,9 +1789,11 @@ void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st) {
   else if (layer == 1) hipLaunchKernelGGL((k_mpnn<1, false>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((k_mpnn<2, false>), grid, dim3(256), 0, st, a);
 }
-void launch_down(int df, const DownArgs& a, bool coop, hipStream_t st) {
+void launch_down(int df, const DownArgs& a, int form, hipStream_t st) {
   dim3 grid((unsigned)((a.n_tiles + 3) / 4));
-  if (df == 1 && coop) hipLaunchKernelGGL(k_down_coop, dim3((unsigned)a.n_tiles), dim3(256), 0, st, a);
+  if (df == 1 && form == DOWN_COOP) hipLaunchKernelGGL(k_down_coop, dim3((unsigned)a.n_tiles), dim3(256), 0, st, a);
+  else if (df == 1 && form == DOWN_PAIR)
+    hipLaunchKernelGGL(k_down_pair, dim3((unsigned)((a.n_tiles + 1) / 2)), dim3(256), 0, st, a);
   else if (df == 1) hipLaunchKernelGGL(k_down<1>, grid, dim3(256), 0, st, a);
   else if (df == 2) hipLaunchKernelGGL(k_down<2>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(k_down<4>, grid, dim3(256), 0, st, a);

@@ -375,7 +375,8 @@ class Tokenizer:
         C = int(out[1])
         names = {0: "fused", 1: "fused_half", 2: "split"}
         return {"ranges": int(out[0]), "chunks": C, "cuts": [int(x) for x in out[2:3 + C]],
-                "schedules": [names[int(x)] for x in out[11:11 + C]]}
+                "schedules": [names[int(x)] for x in out[11:11 + C]],
+                "downsampler": {0: "one_wave", 1: "coop", 2: "pair"}[int(out[19])]}
 
 
 class Decoder:

@@ -256,26 +256,33 @@ def test_fused_and_split_layers_identical(split, half, monkeypatch):
 
 @pytest.mark.parametrize("cb", [4096, 64000])
 def test_down_coop_and_one_wave_identical(cb, monkeypatch):
-    """k_down_coop (four waves per 32-token tile, small batches) and k_down<1> (one wave per
-    tile) give the same bits: tokens, bounded/quantized codes and pre-projection embeddings."""
+    """k_down_coop (four waves per 32-token tile, small batches), k_down_pair (two waves per
+    tile, one track each, one-round batches) and k_down<1> (one wave per tile) give the same bits:
+    tokens, bounded/quantized codes and pre-projection embeddings. Odd tile count (the pair
+    kernel's last workgroup holds one live tile) and ragged proteins."""
     from pst_amd._native import Tokenizer, pack_samples
     samples = [synthetic.synthetic_protein(n, 700 + n) for n in (51, 64, 200, 512, 97)]
     pos, flags, off = pack_samples(samples)
     R = int(off[-1])
     blob = P.random_blob(len(LEVELS[cb]), 77)
     outs = []
-    for coop in ("0", "1000000"):
+    for coop, pair, form in (("0", "0", "one_wave"), ("1000000", "0", "coop"), ("0", "1", "pair")):
         monkeypatch.setenv("PST_DOWN_COOP", coop)
+        monkeypatch.setenv("PST_DOWN_PAIR", pair)
+        monkeypatch.setenv("PST_H2D_CHUNKS", "1")
         tk = Tokenizer(0, cb, 1, blob)
         tok, nt, _ = tk.tokenize_packed(pos, flags, off)
+        assert tk.last_plan_detail()["downsampler"] == form
         outs.append((tok[:R].copy(), tk.aux(R)))
-    (t0, a0), (t1, a1) = outs
-    assert np.array_equal(t0, t1)
-    for k in ("bounded", "quantize", "pre_proj"):
-        assert np.array_equal(a0[k].view(np.uint32), a1[k].view(np.uint32)), k
+        tk.close()
+    t0, a0 = outs[0]
+    for t1, a1 in outs[1:]:
+        assert np.array_equal(t0, t1)
+        for k in ("bounded", "quantize", "pre_proj"):
+            assert np.array_equal(a0[k].view(np.uint32), a1[k].view(np.uint32)), k
     s = samples[3]
     o = O.tokenize(blob, LEVELS[cb], 1, s.atom37_positions, s.atom_flags())
-    assert np.array_equal(t1[off[3]: off[3] + nt[3]], o["tokens"])
+    assert np.array_equal(outs[2][0][off[3]: off[3] + nt[3]], o["tokens"])
 
 
 def test_node_coop_and_one_wave_identical(monkeypatch):
