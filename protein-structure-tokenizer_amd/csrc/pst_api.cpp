@@ -44,11 +44,13 @@ bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
 }
 
 // Downsampler (df 1): a batch of at most this many tiles per SIMD runs k_down_coop (four waves
-// per 32-token tile) instead of k_down (one wave per tile): below that the one-wave kernel
-// leaves most SIMDs idle and its latency is the 20 sequential GEMMs of one wave. Measured
-// (tools/down_coop_ab.sh): 64 tiles 0.34 -> 0.21 ms, 256 tiles 0.41 -> 0.27 ms, 512 tiles equal,
-// 1024 tiles 0.44 -> 0.73 ms.
-constexpr double DOWN_COOP_SIMD_FRACTION = 0.375;
+// per 32-token tile, one wave per SIMD: up to SIMDs/4 tiles in one round) instead of k_down (one
+// wave per tile): below that the one-wave kernel leaves most SIMDs idle and its latency is the 20
+// sequential GEMMs of one wave. Above it, up to one round of tiles, k_down_pair (two waves per
+// tile). Measured (tools/r03_down_forms.sh, profiles/r03_down_forms.jsonl, ms one-wave / coop /
+// pair): 128 tiles 0.405 / 0.203 / 0.278; 384 tiles 0.410 / 0.354 / 0.288; 512 0.417 / 0.354 /
+// 0.295; 768 0.433 / 0.508 / 0.332; 1024 0.447 / 0.656 / 0.357; 2048 0.626 / 1.253 / 0.726.
+constexpr double DOWN_COOP_SIMD_FRACTION = 0.25;
 // Split-schedule node update: k_mpnn_node_coop (four waves per 32 receivers) up to this many
 // tasks per SIMD, k_mpnn_node (one wave) above.
 constexpr double NODE_COOP_SIMD_FRACTION = 0.375;
