@@ -243,6 +243,7 @@ struct pst_ctx {
   int64_t node_coop = -2;    // PST_NODE_COOP: k_mpnn_node_coop iff split and n_tasks <= this; -1 = default
   int64_t down_coop = -2;    // PST_DOWN_COOP: k_down_coop iff n_tiles <= this; -1 = default; -2 = not read yet
   int64_t down_pair = -2;    // PST_DOWN_PAIR: 1 = k_down_pair whenever not coop (df 1), 0 = never; -1 = one round of tiles
+  int32_t* h_counts = nullptr;  // pinned host copy of [n_tok | n_nodes] (cap_B each)
   int32_t last_down_form = 0;  // pst::DOWN_* of the last run (pst_debug_fetch 20, plan[19])
   int64_t half_tasks = -2;   // PST_HALF_TASKS: 1 = fused layers always two waves per task, 0 = never; -1 = policy
   std::vector<int64_t> h_offsets;
@@ -457,8 +458,8 @@ int ensure_workspace(pst_ctx* ctx, int64_t R, int B) {
   };
   auto& w = ctx->w;
   std::vector<Item> items = {
-      {(void**)&w.offsets, sizeof(int64_t) * (B + 1)},   {(void**)&w.n_nodes, sizeof(int32_t) * B},
-      {(void**)&w.n_tok, sizeof(int32_t) * B},          {(void**)&w.tile_prot, sizeof(int32_t) * (Rpad / 32 + B)},
+      {(void**)&w.offsets, sizeof(int64_t) * (B + 1)},   {(void**)&w.n_tok, sizeof(int32_t) * 2 * B},
+      {(void**)&w.tile_prot, sizeof(int32_t) * (Rpad / 32 + B)},
       {(void**)&w.tile_t0, sizeof(int32_t) * (Rpad / 32 + B)},
       {(void**)&w.node_local, sizeof(int32_t) * Rpad}, {(void**)&w.node_prot, sizeof(int32_t) * Rpad},
       {(void**)&w.senders, sizeof(int32_t) * E},        {(void**)&w.deg, sizeof(int32_t) * Rpad},
@@ -487,6 +488,11 @@ int ensure_workspace(pst_ctx* ctx, int64_t R, int B) {
     *it.p = p;
     p += (it.bytes + 4095) / 4096 * 4096;
   }
+  // the per-protein counts side by side, [n_tok (B) | n_nodes (B)]: one D2H for both
+  w.n_nodes = w.n_tok + B;
+  if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
+  ctx->h_counts = nullptr;
+  if (hipHostMalloc((void**)&ctx->h_counts, sizeof(int32_t) * 2 * B) != hipSuccess) ctx->h_counts = nullptr;
   ctx->ws_bytes = total;
   const char* dbg = getenv("PST_DEBUG");
   if (dbg && dbg[0] == '1') {
@@ -856,6 +862,7 @@ int pst_destroy(pst_ctx* ctx) {
   if (ctx->msg) (void)hipFree(ctx->msg);
   for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_U, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
+  if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
   for (hipStream_t cs : {ctx->copy_stream, ctx->copy_stream2})
     if (cs) {
       (void)hipStreamSynchronize(cs);
@@ -1065,11 +1072,23 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
   }
   hipLaunchKernelGGL(k_ntok, dim3((n_prot + 255) / 256), dim3(256), 0, ctx->stream, w.n_nodes, w.n_tok, n_prot, ctx->df);
   HIPCHK(hipMemcpyAsync(tokens_out, w.tokens, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, ctx->stream));
-  if (n_tokens_out)
-    HIPCHK(hipMemcpyAsync(n_tokens_out, w.n_tok, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
-  if (n_nodes_out)
-    HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
+  // both count arrays in one copy into pinned memory (one DMA instead of two staged ones)
+  const bool counts = n_tokens_out || n_nodes_out;
+  const int64_t capB = ctx->cap_B;
+  if (counts && ctx->h_counts)
+    HIPCHK(hipMemcpyAsync(ctx->h_counts, w.n_tok, sizeof(int32_t) * (capB + n_prot), hipMemcpyDeviceToHost,
+                          ctx->stream));
+  else if (counts) {
+    if (n_tokens_out)
+      HIPCHK(hipMemcpyAsync(n_tokens_out, w.n_tok, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
+    if (n_nodes_out)
+      HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
+  }
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (counts && ctx->h_counts) {
+    if (n_tokens_out) std::memcpy(n_tokens_out, ctx->h_counts, sizeof(int32_t) * n_prot);
+    if (n_nodes_out) std::memcpy(n_nodes_out, ctx->h_counts + capB, sizeof(int32_t) * n_prot);
+  }
   return PST_OK;
 }
 
