@@ -613,7 +613,8 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
                                                   float* __restrict__ feat /*[N][2112]*/, DecBatch bt,
                                                   const float* __restrict__ kT_all /*[192][Ntot]*/,
                                                   const float* __restrict__ kpT_all /*[144][Ntot]*/, int Ntot,
-                                                  int ld /*row stride of qs and kvs*/) {
+                                                  int ld /*row stride of qs and kvs*/,
+                                                  float* __restrict__ att_out /*[pairs][12] or null*/) {
   __shared__ float attT[512 * ATT_LD];
   __shared__ float res_pt[12 * 8 * 3];
   const int64_t ig = blockIdx.x;
@@ -636,6 +637,11 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   __syncthreads();
   const float* kT = kT_all + n0;  // column j = key j of this protein
   const float* kpT = kpT_all + n0;
+#ifdef PST_EXP_NO_IPA_LOGITS  // timing-only ablation (results differ): logits = pair bias only
+  for (int j = tid; j < N; j += 256)
+    for (int h = 0; h < 12; ++h) attT[j * ATT_LD + h] = b2d[(int64_t)j * 12 + h];
+  if (false)
+#endif
   for (int j = tid; j < N; j += 256) {
     const float4* brow = reinterpret_cast<const float4*>(b2d + (int64_t)j * 12);
     float bb[12];
@@ -686,7 +692,17 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   }
   __syncthreads();
   float* f = feat + ig * 2112;
-  if (MFMA_PAIR) {
+  if (MFMA_PAIR && att_out) {
+    // the attention weights of query i for k_ipa_values: att_out[(pair row (i, j)) * 12 + h]
+    float* ao = att_out + (bt.pair_off[bprot] + (int64_t)il * N) * 12;
+    for (int e = tid; e < N * 12; e += 256) ao[e] = attT[(e / 12) * ATT_LD + e % 12];
+  }
+#ifdef PST_EXP_NO_IPA_PAIR  // timing-only ablation (results differ): skip the pair sums
+  if (false)
+#else
+  if (MFMA_PAIR)
+#endif
+  {
     // pair attention on the matrix cores: lane (i = lane & 15, g = lane >> 4) feeds A = z[4s+g][c0+i]
     // and B = att[head i][4s+g] (0 for the 4 padding heads); after the chain it holds
     // D[c0 + 4g + r][head i], r = 0..3
@@ -698,17 +714,17 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
     const float* zrow = zln + (int64_t)g * 128;
     int s = 0;
     const int S = N / 4;  // whole k-steps; a tail of N % 4 keys runs as one zero-padded step
-    for (; s + 4 <= S; s += 4) {
-      float za[4], zb[4], bt4[4];
+    for (; s + 8 <= S; s += 8) {  // 8 k-steps of z loads in flight per trip
+      float za[8], zb[8], bt4[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const float* zr = zrow + (int64_t)(4 * (s + u)) * 128;
         za[u] = zr[cA];
         zb[u] = zr[cB];
         bt4[u] = hv ? attT[(4 * (s + u) + g) * ATT_LD + i] : 0.0f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         accA = __builtin_amdgcn_mfma_f32_16x16x4f32(za[u], bt4[u], accA, 0, 0, 0);
         accB = __builtin_amdgcn_mfma_f32_16x16x4f32(zb[u], bt4[u], accB, 0, 0, 0);
       }
@@ -729,6 +745,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
       *reinterpret_cast<float4*>(o + 16) = make_float4(accB[0], accB[1], accB[2], accB[3]);
     }
   }
+  if (MFMA_PAIR && att_out) return;  // value sums and the local frames: k_ipa_values, k_ipa_local
   // Value sums (and, without MFMA_PAIR, the pair attention): per thread the value outputs
   // o = tid and tid + 256 (scalar values 0..191, global value points 192..479) and, VALU form, the
   // pair attention of channel c for heads hg, hg+2, ... (6 sums). Each sum is its own in-order
@@ -758,6 +775,9 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
     float pacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float vacc[2] = {0.f, 0.f};
     int j = 0;
+#ifdef PST_EXP_NO_IPA_VALUES  // timing-only ablation (results differ): skip the value sums
+    if (MFMA_PAIR) j = N;
+#endif
     for (; j + 8 <= N; j += 8) {
       float zv[8], v0[8], v1[8];
 #pragma unroll
@@ -816,6 +836,85 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
     f[384 + tid] = lz;
     f[480 + tid] = sqrtf(((1e-8f + lx * lx) + ly * ly) + lz * lz);
   }
+}
+
+// IPA value sums, batched over queries (the per-query form re-read every key's values from L2:
+// 1 GB per fold iteration at 8 x 256 residues). One wave per (16 queries of one protein, head h):
+// D[q][o] = Σ_j att[q][h][j] · V_h[j][o] on v_mfma_f32_16x16x4_f32 for the 16 scalar values and
+// the 8 value points × xyz (24) of head h — three 16-wide output blocks (8 columns unused). The
+// instruction is a k-ascending fmaf chain, so each sum is the in-order chain over j from 0 that
+// k_ipa_attn<false> runs per query: identical bits. Scalar outputs go to feat[q][16h + o], the
+// global-frame points to vpt[q][24h + o'] for k_ipa_local.
+__global__ __launch_bounds__(64) void k_ipa_values(const float* __restrict__ att_all, const float* __restrict__ kvs_all,
+                                                   const float* __restrict__ kvpg_all, float* __restrict__ feat,
+                                                   float* __restrict__ vpt, DecBatch bt,
+                                                   const int32_t* __restrict__ vt_prot,
+                                                   const int32_t* __restrict__ vt_q0, int ld) {
+  const int tile = blockIdx.x, h = blockIdx.y;
+  const int lane = threadIdx.x, i = lane & 15, g = lane >> 4;
+  const int b = vt_prot[tile], q0 = vt_q0[tile];
+  const int64_t n0 = bt.node_off[b];
+  const int N = (int)(bt.node_off[b + 1] - n0);
+  const int qa = q0 + i;  // A-operand row (query) of this lane
+  const int qc = qa < N ? qa : N - 1;
+  const float* arow = att_all + (bt.pair_off[b] + (int64_t)qc * N) * 12 + h;
+  const float* vs = kvs_all + n0 * ld + h * 32 + 16 + i;
+  const float* vp = kvpg_all + n0 * 432 + (h * 12 + 4) * 3 + i;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0;
+  // 8 k-steps of operands loaded per trip, then their 24 MFMAs (one memory round trip per 32 keys;
+  // 16 per trip measured slower: 183 -> 202 us per 8 x 256 decode)
+  const int S = (N + 3) / 4;
+  for (int s0 = 0; s0 < S; s0 += 8) {
+    float a[8], b0[8], b1[8], b2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = 4 * (s0 + u) + g;
+      const bool jv = j < N;
+      a[u] = jv ? arow[(int64_t)j * 12] : 0.0f;
+      b0[u] = jv ? vs[(int64_t)j * ld] : 0.0f;
+      b1[u] = jv ? vp[(int64_t)j * 432] : 0.0f;
+      b2[u] = jv && i < 8 ? vp[(int64_t)j * 432 + 16] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b0[u], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b1[u], acc1, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b2[u], acc2, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = q0 + 4 * g + r;
+    if (q >= N) continue;
+    const int64_t row = n0 + q;
+    feat[row * 2112 + h * 16 + i] = acc0[r];
+    vpt[row * 288 + h * 24 + i] = acc1[r];
+    if (i < 8) vpt[row * 288 + h * 24 + 16 + i] = acc2[r];
+  }
+}
+
+// Value points of query i from the global frame to its local frame (invert_point) and their norms
+// (folding.py:256-275), after k_ipa_values.
+__global__ void k_ipa_local(const float* __restrict__ vpt, const float* __restrict__ aff,
+                            const float* __restrict__ rot, float* __restrict__ feat, int N) {
+  const int64_t ig = blockIdx.x;
+  const int tid = threadIdx.x;  // 96
+  if (ig >= N) return;
+  const float* res_pt = vpt + ig * 288;
+  float* f = feat + ig * 2112;
+  const int h = tid / 8, p = tid % 8;
+  const float* R = rot + ig * 9;
+  const float* tr = aff + ig * 7 + 4;
+  const float gx = res_pt[(h * 8 + p) * 3 + 0] - tr[0];
+  const float gy = res_pt[(h * 8 + p) * 3 + 1] - tr[1];
+  const float gz = res_pt[(h * 8 + p) * 3 + 2] - tr[2];
+  const float lx = R[0] * gx + R[3] * gy + R[6] * gz;
+  const float ly = R[1] * gx + R[4] * gy + R[7] * gz;
+  const float lz = R[2] * gx + R[5] * gy + R[8] * gz;
+  f[192 + tid] = lx;
+  f[288 + tid] = ly;
+  f[384 + tid] = lz;
+  f[480 + tid] = sqrtf(((1e-8f + lx * lx) + ly * ly) + lz * lz);
 }
 
 // Backbone torsions → frames → atom14 → atom37 (folding.py:674-746, all_atom.py:473-595, :122-135)
@@ -1112,7 +1211,8 @@ struct Scratch {
   float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
   float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *kT, *kpT, *init_relu, *ipa_in;
   int64_t *tok_off, *node_off, *pair_off;
-  int32_t *tok_prot, *node_prot;
+  int32_t *tok_prot, *node_prot, *vt_prot, *vt_q0;
+  float *att, *vpt;
   uint32_t* tokens;
 };
 
@@ -1144,7 +1244,9 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
                 {(void**)&S->init_relu, NN * 128 * F},
                 {(void**)&S->tok_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->node_off, (NN + 1) * sizeof(int64_t)},
                 {(void**)&S->pair_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->tok_prot, NN * sizeof(int32_t)},
-                {(void**)&S->node_prot, NN * sizeof(int32_t)}, {(void**)&S->tokens, NN * sizeof(uint32_t)}};
+                {(void**)&S->node_prot, NN * sizeof(int32_t)}, {(void**)&S->tokens, NN * sizeof(uint32_t)},
+                {(void**)&S->vt_prot, 2 * NN * sizeof(int32_t)}, {(void**)&S->vt_q0, 2 * NN * sizeof(int32_t)},
+                {(void**)&S->att, NP * 12 * F}, {(void**)&S->vpt, NN * 288 * F}};
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 255) / 256 * 256;
   if (!dec->ws) {
@@ -1167,7 +1269,7 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
 // Host view of one group: proteins [b0, b1) of the call.
 struct Group {
   std::vector<int64_t> tok_off, node_off, pair_off;
-  std::vector<int32_t> tok_prot, node_prot;
+  std::vector<int32_t> tok_prot, node_prot, vt_prot, vt_q0;  // k_ipa_values tiles: 16 queries of one protein
   std::vector<uint32_t> tokens;
   int64_t T = 0, N = 0, NP = 0;
   int B = 0;
@@ -1185,6 +1287,15 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   DCHK(hipMemcpyAsync(S.pair_off, G.pair_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
   DCHK(hipMemcpyAsync(S.tok_prot, G.tok_prot.data(), sizeof(int32_t) * T, hipMemcpyHostToDevice, st));
   DCHK(hipMemcpyAsync(S.node_prot, G.node_prot.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
+  std::vector<int32_t> vt_prot, vt_q0;
+  for (int b = 0; b < G.B; ++b)
+    for (int64_t q0 = 0; q0 < G.node_off[b + 1] - G.node_off[b]; q0 += 16) {
+      vt_prot.push_back(b);
+      vt_q0.push_back((int32_t)q0);
+    }
+  const int n_vt = (int)vt_prot.size();
+  DCHK(hipMemcpyAsync(S.vt_prot, vt_prot.data(), sizeof(int32_t) * n_vt, hipMemcpyHostToDevice, st));
+  DCHK(hipMemcpyAsync(S.vt_q0, vt_q0.data(), sizeof(int32_t) * n_vt, hipMemcpyHostToDevice, st));
   DecBatch bt{G.B, S.tok_off, S.node_off, S.pair_off, S.tok_prot, S.node_prot};
   const int Ni = (int)N;
   // ---- upsampler (CrossAttentionScaler, use_original_posenc)
@@ -1263,7 +1374,13 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     hipLaunchKernelGGL(k_ipa_points, dim3((unsigned)N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg,
                        S.kvs, S.kT, S.kpT, Ni, 1152);
     hipLaunchKernelGGL(ipa_mfma ? k_ipa_attn<true> : k_ipa_attn<false>, dim3((unsigned)N), dim3(256), 0, st, S.qs,
-                       S.kvs, S.qpg, S.kvpg, S.b2d, S.zln, dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152);
+                       S.kvs, S.qpg, S.kvpg, S.b2d, S.zln, dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152,
+                       ipa_mfma ? S.att : nullptr);
+    if (ipa_mfma) {
+      hipLaunchKernelGGL(k_ipa_values, dim3((unsigned)n_vt, 12), dim3(64), 0, st, S.att, S.kvs, S.kvpg, S.feat, S.vpt,
+                         bt, S.vt_prot, S.vt_q0, 1152);
+      hipLaunchKernelGGL(k_ipa_local, dim3((unsigned)N), dim3(96), 0, st, S.vpt, S.aff, S.rot, S.feat, Ni);
+    }
     gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
     layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
     gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
