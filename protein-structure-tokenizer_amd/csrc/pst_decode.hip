@@ -1046,6 +1046,8 @@ struct pst_decoder {
   size_t ws_bytes = 0;
   // last call's intermediates (per protein offsets) for pst_decoder_debug
   std::vector<float> last_single, last_pair, last_traj, last_angles, last_atom14;
+  // decode_group's kernel sequence as HIP graphs, keyed by the group's shape (decode_group)
+  std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
 };
 
 namespace {
@@ -1298,114 +1300,153 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   DCHK(hipMemcpyAsync(S.vt_q0, vt_q0.data(), sizeof(int32_t) * n_vt, hipMemcpyHostToDevice, st));
   DecBatch bt{G.B, S.tok_off, S.node_off, S.pair_off, S.tok_prot, S.node_prot};
   const int Ni = (int)N;
-  // ---- upsampler (CrossAttentionScaler, use_original_posenc)
-  hipLaunchKernelGGL(k_up_init, dim3((unsigned)T), dim3(128), 0, st, S.tokens, bt, T, dec->d_levels, dec->D,
-                     W.up_proj.w, W.up_proj.b, dec->d_pe_tok, S.orig_in);
-  gemm(st, S.orig_in, 256, W.proj_original, S.orig, 128, (int)T, 0);
-  hipLaunchKernelGGL(k_node_pe, dim3((unsigned)N), dim3(128), 0, st, dec->d_pe_node, bt, N, S.res);
-  for (int b = 0; b < 3; ++b) {
-    layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.qn[b]);
-    layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.dn[b]);
-    gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, Ni, 0);
-    gemm_raw(st, S.ln_a, 128, W.wg[b], 128, 128, W.gb[b], S.gate, 128, Ni, F_SIGMOID_OUT);
-    gemm_raw(st, S.ln_b, 128, W.wk[b], 128, 128, nullptr, S.k, 128, (int)T, 0);
-    gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, (int)T, 0);
-    // q · key_dim^-0.5 (modules.py:346)
-    hipLaunchKernelGGL(k_scale, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.q, N * 128,
-                       0.176776695296637f);
-    hipLaunchKernelGGL(k_up_attn, dim3((unsigned)N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, bt, N);
-    gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, Ni, F_ACCUM);
-    layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.rt_ln[b]);
-    gemm(st, S.ln_a, 128, W.rt1[b], S.tr_h, 256, Ni, F_RELU_OUT);
-    gemm(st, S.tr_h, 256, W.rt2[b], S.res, 128, Ni, F_ACCUM);
-    layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.ot_ln[b]);
-    gemm(st, S.ln_b, 128, W.ot1[b], S.tr_h, 256, (int)T, F_RELU_OUT);
-    gemm(st, S.tr_h, 256, W.ot2[b], S.orig, 128, (int)T, F_ACCUM);
-  }
-  hipLaunchKernelGGL(k_spherical, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.res, Ni);  // s_i
-  // ---- sequence decoder: pair representation over each protein's N_b² pairs
-  const int NPi = (int)NP;
-  layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.pr_ln_in);
-  gemm(st, S.ln_a, 128, W.left, S.left, 256, Ni, 0);
-  gemm(st, S.ln_a, 128, W.right, S.right, 256, Ni, 0);
   const bool fused = !getenv("PST_DECODE_UNFUSED");
   const bool ipa_mfma = !getenv("PST_DECODE_IPA_VALU");  // A/B: the VALU pair sum (same bits)
-  if (fused) {
-    layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
-    gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
-    PairArgs pa = dec->pair;
-    pa.left = S.left;
-    pa.right = S.right;
-    pa.z = keep_debug ? S.z : nullptr;
-    pa.zln = S.zln;
-    pa.b2d = S.b2d;
-    pa.NP = NP;
-    pa.bt = bt;
-    const int64_t tiles = (NP + 31) / 32;
-    hipLaunchKernelGGL(k_pair_fused, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, pa);
-  } else {
-    hipLaunchKernelGGL(k_pair_product, dim3((unsigned)NP), dim3(256), 0, st, S.left, S.right, S.P, bt);
-    gemm(st, S.P, 256, W.out1, S.h1, 256, NPi, F_RELU_OUT);
-    gemm(st, S.h1, 256, W.out2, S.pair0, 128, NPi, 0);
-    gemm(st, S.P, 256, W.right1, S.lin_out, 128, NPi, 0);
-    hipLaunchKernelGGL(k_add, dim3((unsigned)((NP * 128 + 255) / 256)), dim3(256), 0, st, S.pair0, S.lin_out, NP * 128);
-    layernorm(st, S.pair0, 128, S.pair0, 128, NPi, 128, W.pr_ln_out);
-    hipLaunchKernelGGL(k_pair_concat, dim3((unsigned)NP), dim3(128), 0, st, dec->d_pe_rel, S.pair0, S.catb, bt);
-    gemm(st, S.catb, 256, W.seq_linear, S.lin_out, 128, NPi, 0);
-    layernorm(st, S.lin_out, 128, S.lnz, 128, NPi, 128, W.pt_ln);
-    gemm(st, S.lnz, 128, W.pt1, S.h1, 256, NPi, F_RELU_OUT);
-    gemm(st, S.h1, 256, W.pt2, S.z, 128, NPi, 0);  // z_ij (Transition output, no residual)
-    // ---- structure module
-    layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
-    gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
-    layernorm(st, S.z, 128, S.zln, 128, NPi, 128, W.pair_ln);
-    gemm(st, S.zln, 128, W.att2d, S.b2d, 12, NPi, 0);
-    hipLaunchKernelGGL(k_scale, dim3((unsigned)((NP * 12 + 255) / 256)), dim3(256), 0, st, S.b2d, NP * 12,
-                       0.577350269189626f);
-  }
-  hipLaunchKernelGGL(k_affine_init, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, Ni);
-  // relu(init_act) feeds the angle resnet of every iteration: once, not 8 copies
-  hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.init_act, 128, S.init_relu,
-                     (int64_t)Ni, 128);
-  for (int it = 0; it < 8; ++it) {
-    // the four IPA input projections as one 384 -> 1152 GEMM: [q_scalar | kv_scalar | q_point |
-    // kv_point] columns of ipa_in (row stride 1152)
-    gemm_raw(st, S.act, 384, dec->d_ipa_w, 384, 1152, dec->d_ipa_b, S.ipa_in, 1152, Ni, 0);
-    hipLaunchKernelGGL(k_ipa_points, dim3((unsigned)N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg,
-                       S.kvs, S.kT, S.kpT, Ni, 1152);
-    hipLaunchKernelGGL(ipa_mfma ? k_ipa_attn<true> : k_ipa_attn<false>, dim3((unsigned)N), dim3(256), 0, st, S.qs,
-                       S.kvs, S.qpg, S.kvpg, S.b2d, S.zln, dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152,
-                       ipa_mfma ? S.att : nullptr);
-    if (ipa_mfma) {
-      hipLaunchKernelGGL(k_ipa_values, dim3((unsigned)n_vt, 12), dim3(64), 0, st, S.att, S.kvs, S.kvpg, S.feat, S.vpt,
-                         bt, S.vt_prot, S.vt_q0, 1152);
-      hipLaunchKernelGGL(k_ipa_local, dim3((unsigned)N), dim3(96), 0, st, S.vpt, S.aff, S.rot, S.feat, Ni);
+  auto launch = [&]() -> int {
+    // ---- upsampler (CrossAttentionScaler, use_original_posenc)
+    hipLaunchKernelGGL(k_up_init, dim3((unsigned)T), dim3(128), 0, st, S.tokens, bt, T, dec->d_levels, dec->D,
+                       W.up_proj.w, W.up_proj.b, dec->d_pe_tok, S.orig_in);
+    gemm(st, S.orig_in, 256, W.proj_original, S.orig, 128, (int)T, 0);
+    hipLaunchKernelGGL(k_node_pe, dim3((unsigned)N), dim3(128), 0, st, dec->d_pe_node, bt, N, S.res);
+    for (int b = 0; b < 3; ++b) {
+      layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.qn[b]);
+      layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.dn[b]);
+      gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, Ni, 0);
+      gemm_raw(st, S.ln_a, 128, W.wg[b], 128, 128, W.gb[b], S.gate, 128, Ni, F_SIGMOID_OUT);
+      gemm_raw(st, S.ln_b, 128, W.wk[b], 128, 128, nullptr, S.k, 128, (int)T, 0);
+      gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, (int)T, 0);
+      // q · key_dim^-0.5 (modules.py:346)
+      hipLaunchKernelGGL(k_scale, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.q, N * 128,
+                         0.176776695296637f);
+      hipLaunchKernelGGL(k_up_attn, dim3((unsigned)N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, bt, N);
+      gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, Ni, F_ACCUM);
+      layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.rt_ln[b]);
+      gemm(st, S.ln_a, 128, W.rt1[b], S.tr_h, 256, Ni, F_RELU_OUT);
+      gemm(st, S.tr_h, 256, W.rt2[b], S.res, 128, Ni, F_ACCUM);
+      layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.ot_ln[b]);
+      gemm(st, S.ln_b, 128, W.ot1[b], S.tr_h, 256, (int)T, F_RELU_OUT);
+      gemm(st, S.tr_h, 256, W.ot2[b], S.orig, 128, (int)T, F_ACCUM);
     }
-    gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
-    layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
-    gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
-    gemm(st, S.tmp384a, 384, W.tr[1], S.tmp384b, 384, Ni, F_RELU_OUT);
-    gemm(st, S.tmp384b, 384, W.tr[2], S.act, 384, Ni, F_ACCUM);  // += input_act
-    layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.tr_ln);
-    gemm(st, S.act, 384, W.affine_update, S.upd, 6, Ni, 0);
-    hipLaunchKernelGGL(k_affine_update, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.upd, Ni);
-    // MultiRigidSidechain: (0 + Lin(relu(act))) + Lin(relu(initial_act)), 2 residual blocks, angles
-    hipLaunchKernelGGL(k_zero, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.sca, N * 128);
-    gemm(st, S.act, 384, W.sc_in, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
-    gemm(st, S.init_relu, 128, W.sc_in1, S.sca, 128, Ni, F_ACCUM);
-    // scb is only ever read through a ReLU: apply it in the producing GEMM's epilogue instead of
-    // as a copy before the consumer (same values)
-    gemm(st, S.sca, 128, W.rb1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
-    gemm(st, S.scb, 128, W.rb2, S.sca, 128, Ni, F_ACCUM);
-    gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
-    gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, Ni, F_ACCUM);
-    gemm(st, S.sca, 128, W.angles, S.unnorm, 6, Ni, F_RELU_IN);
-    const bool last = it == 7;
-    hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.unnorm,
-                       S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7, last ? S.atom37 : nullptr,
-                       last ? S.atom14 : nullptr, Ni);
+    hipLaunchKernelGGL(k_spherical, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.res, Ni);  // s_i
+    // ---- sequence decoder: pair representation over each protein's N_b² pairs
+    const int NPi = (int)NP;
+    layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.pr_ln_in);
+    gemm(st, S.ln_a, 128, W.left, S.left, 256, Ni, 0);
+    gemm(st, S.ln_a, 128, W.right, S.right, 256, Ni, 0);
+    if (fused) {
+      layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
+      gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
+      PairArgs pa = dec->pair;
+      pa.left = S.left;
+      pa.right = S.right;
+      pa.z = keep_debug ? S.z : nullptr;
+      pa.zln = S.zln;
+      pa.b2d = S.b2d;
+      pa.NP = NP;
+      pa.bt = bt;
+      const int64_t tiles = (NP + 31) / 32;
+      hipLaunchKernelGGL(k_pair_fused, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, pa);
+    } else {
+      hipLaunchKernelGGL(k_pair_product, dim3((unsigned)NP), dim3(256), 0, st, S.left, S.right, S.P, bt);
+      gemm(st, S.P, 256, W.out1, S.h1, 256, NPi, F_RELU_OUT);
+      gemm(st, S.h1, 256, W.out2, S.pair0, 128, NPi, 0);
+      gemm(st, S.P, 256, W.right1, S.lin_out, 128, NPi, 0);
+      hipLaunchKernelGGL(k_add, dim3((unsigned)((NP * 128 + 255) / 256)), dim3(256), 0, st, S.pair0, S.lin_out, NP * 128);
+      layernorm(st, S.pair0, 128, S.pair0, 128, NPi, 128, W.pr_ln_out);
+      hipLaunchKernelGGL(k_pair_concat, dim3((unsigned)NP), dim3(128), 0, st, dec->d_pe_rel, S.pair0, S.catb, bt);
+      gemm(st, S.catb, 256, W.seq_linear, S.lin_out, 128, NPi, 0);
+      layernorm(st, S.lin_out, 128, S.lnz, 128, NPi, 128, W.pt_ln);
+      gemm(st, S.lnz, 128, W.pt1, S.h1, 256, NPi, F_RELU_OUT);
+      gemm(st, S.h1, 256, W.pt2, S.z, 128, NPi, 0);  // z_ij (Transition output, no residual)
+      // ---- structure module
+      layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
+      gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
+      layernorm(st, S.z, 128, S.zln, 128, NPi, 128, W.pair_ln);
+      gemm(st, S.zln, 128, W.att2d, S.b2d, 12, NPi, 0);
+      hipLaunchKernelGGL(k_scale, dim3((unsigned)((NP * 12 + 255) / 256)), dim3(256), 0, st, S.b2d, NP * 12,
+                         0.577350269189626f);
+    }
+    hipLaunchKernelGGL(k_affine_init, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, Ni);
+    // relu(init_act) feeds the angle resnet of every iteration: once, not 8 copies
+    hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.init_act, 128, S.init_relu,
+                       (int64_t)Ni, 128);
+    for (int it = 0; it < 8; ++it) {
+      // the four IPA input projections as one 384 -> 1152 GEMM: [q_scalar | kv_scalar | q_point |
+      // kv_point] columns of ipa_in (row stride 1152)
+      gemm_raw(st, S.act, 384, dec->d_ipa_w, 384, 1152, dec->d_ipa_b, S.ipa_in, 1152, Ni, 0);
+      hipLaunchKernelGGL(k_ipa_points, dim3((unsigned)N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg,
+                         S.kvs, S.kT, S.kpT, Ni, 1152);
+      hipLaunchKernelGGL(ipa_mfma ? k_ipa_attn<true> : k_ipa_attn<false>, dim3((unsigned)N), dim3(256), 0, st, S.qs,
+                         S.kvs, S.qpg, S.kvpg, S.b2d, S.zln, dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152,
+                         ipa_mfma ? S.att : nullptr);
+      if (ipa_mfma) {
+        hipLaunchKernelGGL(k_ipa_values, dim3((unsigned)n_vt, 12), dim3(64), 0, st, S.att, S.kvs, S.kvpg, S.feat, S.vpt,
+                           bt, S.vt_prot, S.vt_q0, 1152);
+        hipLaunchKernelGGL(k_ipa_local, dim3((unsigned)N), dim3(96), 0, st, S.vpt, S.aff, S.rot, S.feat, Ni);
+      }
+      gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
+      layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
+      gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
+      gemm(st, S.tmp384a, 384, W.tr[1], S.tmp384b, 384, Ni, F_RELU_OUT);
+      gemm(st, S.tmp384b, 384, W.tr[2], S.act, 384, Ni, F_ACCUM);  // += input_act
+      layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.tr_ln);
+      gemm(st, S.act, 384, W.affine_update, S.upd, 6, Ni, 0);
+      hipLaunchKernelGGL(k_affine_update, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.upd, Ni);
+      // MultiRigidSidechain: (0 + Lin(relu(act))) + Lin(relu(initial_act)), 2 residual blocks, angles
+      hipLaunchKernelGGL(k_zero, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.sca, N * 128);
+      gemm(st, S.act, 384, W.sc_in, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
+      gemm(st, S.init_relu, 128, W.sc_in1, S.sca, 128, Ni, F_ACCUM);
+      // scb is only ever read through a ReLU: apply it in the producing GEMM's epilogue instead of
+      // as a copy before the consumer (same values)
+      gemm(st, S.sca, 128, W.rb1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
+      gemm(st, S.scb, 128, W.rb2, S.sca, 128, Ni, F_ACCUM);
+      gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
+      gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, Ni, F_ACCUM);
+      gemm(st, S.sca, 128, W.angles, S.unnorm, 6, Ni, F_RELU_IN);
+      const bool last = it == 7;
+      hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.unnorm,
+                         S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7, last ? S.atom37 : nullptr,
+                         last ? S.atom14 : nullptr, Ni);
+    }
+
+    DCHK(hipGetLastError());
+    return PST_OK;
+  };
+  // The ~200 launches of one group are captured once per group shape into a HIP graph and
+  // replayed (the decode was partly launch-bound: kernel time 5.0 ms of ~5.7 ms per 8 x 256
+  // decode). Inputs are uploaded above, outside the graph; every kernel argument is a function of
+  // the shape (per-protein token / node counts) and the decoder's fixed buffers.
+  const bool use_graph = !keep_debug && !getenv("PST_DECODE_NO_GRAPH");
+  if (!use_graph) {
+    int rc = launch();
+    if (rc) return rc;
+  } else {
+    std::vector<int64_t> key{(int64_t)t_mfma, (int64_t)fused, (int64_t)ipa_mfma, G.B};
+    key.insert(key.end(), G.node_off.begin(), G.node_off.end());
+    key.insert(key.end(), G.tok_off.begin(), G.tok_off.end());
+    auto it = dec->graphs.find(key);
+    if (it == dec->graphs.end()) {
+      if (dec->graphs.size() >= 16) {  // bounded cache: start over
+        for (auto& kv : dec->graphs) (void)hipGraphExecDestroy(kv.second);
+        dec->graphs.clear();
+      }
+      DCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      const int rc = launch();
+      hipGraph_t graph = nullptr;
+      const hipError_t ec = hipStreamEndCapture(st, &graph);
+      if (rc) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+      }
+      DCHK(ec);
+      hipGraphExec_t exec = nullptr;
+      const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      DCHK(ei);
+      it = dec->graphs.emplace(key, exec).first;
+    }
+    DCHK(hipGraphLaunch(it->second, st));
   }
-  DCHK(hipGetLastError());
   if (keep_debug) {
     std::vector<float> h((size_t)NP * 128 > (size_t)8 * N * 7 ? (size_t)NP * 128 : (size_t)8 * N * 7);
     auto grab = [&](const float* src, size_t n) -> int {
@@ -1611,6 +1652,8 @@ int pst_decoder_destroy(pst_decoder* dec) {
                   (void*)dec->d_pe_rel, (void*)dec->d_pw, (void*)dec->d_pair, dec->ws, (void*)dec->d_ipa_w,
                   (void*)dec->d_ipa_b})
     if (p) (void)hipFree(p);
+  for (auto& kv : dec->graphs) (void)hipGraphExecDestroy(kv.second);
+  dec->graphs.clear();
   if (dec->stream) (void)hipStreamDestroy(dec->stream);
   delete dec;
   return PST_OK;
