@@ -281,6 +281,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
 }
+// a resource whose accesses are all out of range when p is null (stores dropped, loads read 0)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_or_null(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? 0x7fffffff : 0, 0x00020000);
+}
 __device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
   u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
@@ -402,6 +406,38 @@ __device__ __forceinline__ void tile_gemm_f(Tile& acc, const Tile& X, const floa
     __builtin_amdgcn_sched_barrier(0);
     bq[0] = bn[0];
     bq[1] = bn[1];
+  }
+}
+
+// acc += X · W (tile_gemm) that also writes X out blocked (tile_store_blk layout) through `st`:
+// quad i of X leaves at k-step 4i, the first k-step that reads it. On gfx9 the vector memory
+// counter covers stores and loads in issue order, so a 16-store burst ahead of a GEMM makes the
+// GEMM's first fragment loads wait for every store's write acknowledgement; spread one per group
+// of four k-steps, each store is >= 4 k-steps older than the load whose wait would cover it.
+// Same MFMA chain as tile_gemm: same bits. A null `st` (num_records 0) drops the stores.
+__device__ __forceinline__ void tile_gemm_store(Tile& acc, const Tile& X, const float4* __restrict__ Wf,
+                                                __amdgpu_buffer_rsrc_t st) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
+  const int vo = lane_id() * 16;
+  float4 ring[GEMM_DEPTH];
+#pragma unroll
+  for (int i = 0; i < GEMM_DEPTH; ++i) ring[i] = buf_load4(rs, vo, i * 1024);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    buf_store4(st, vo, g * 1024, X.m[g / 4][4 * (g % 4)], X.m[g / 4][4 * (g % 4) + 1], X.m[g / 4][4 * (g % 4) + 2],
+               X.m[g / 4][4 * (g % 4) + 3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = 4 * g + j;
+      float4 a = ring[t % GEMM_DEPTH];
+      if (t + GEMM_DEPTH < 64) ring[t % GEMM_DEPTH] = buf_load4(rs, vo, (t + GEMM_DEPTH) * 1024);
+      const float b = X.m[t / 16][t % 16];
+      acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b, acc.m[0], 0, 0, 0);
+      acc.m[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b, acc.m[1], 0, 0, 0);
+      acc.m[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b, acc.m[2], 0, 0, 0);
+      acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b, acc.m[3], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 

@@ -24,6 +24,22 @@
 
 namespace pst {
 
+// Diagnostic build only (-DPST_STAMP): per-phase wave cycles of the fused k_mpnn, summed over
+// waves (s_memtime deltas; pst_debug_stamps reads them). Not in the product build.
+#ifdef PST_STAMP
+__device__ unsigned long long g_stamps[3][8];
+#define STAMP(i)                                                        \
+  if (stp) {                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                  \
+    const uint64_t _t = __builtin_amdgcn_s_memtime();                   \
+    stp[i] += _t - stp[7];                                              \
+    stp[7] = _t;                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                  \
+  }
+#else
+#define STAMP(i) (void)stp
+#endif
+
 #ifndef MPNN_MIN_BLOCKS
 #define MPNN_MIN_BLOCKS 2
 #endif
@@ -553,7 +569,11 @@ __device__ __forceinline__ void agg_from_gsum(Tile& ag, const float* __restrict_
 #ifndef FEAT_KSTEPS
 #define FEAT_KSTEPS 15
 #endif
-__device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const float4* __restrict__ Wf) {
+// ST: also write tile E out blocked through `st`, quad r at k-step r (the rest after the loop),
+// spread as in tile_gemm_store
+template <bool ST>
+__device__ __forceinline__ void feat_gemm_st(Tile& acc, const float (&x)[16], const float4* __restrict__ Wf,
+                                             const Tile* E, __amdgpu_buffer_rsrc_t st) {
   __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
   const int vo = lane_id() * 16;
   float4 ring[FEAT_DEPTH];
@@ -561,6 +581,9 @@ __device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const
   for (int i = 0; i < FEAT_DEPTH; ++i) ring[i] = buf_load4(rs, vo, i * 1024);
 #pragma unroll
   for (int r = 0; r < FEAT_KSTEPS; ++r) {
+    if (ST)
+      buf_store4(st, vo, r * 1024, E->m[r / 4][4 * (r % 4)], E->m[r / 4][4 * (r % 4) + 1], E->m[r / 4][4 * (r % 4) + 2],
+                 E->m[r / 4][4 * (r % 4) + 3]);
     const float4 wa = ring[r % FEAT_DEPTH];
     if (r + FEAT_DEPTH < FEAT_KSTEPS) ring[r % FEAT_DEPTH] = buf_load4(rs, vo, (r + FEAT_DEPTH) * 1024);
     acc.m[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, x[r], acc.m[0], 0, 0, 0);
@@ -569,6 +592,14 @@ __device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const
     acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, x[r], acc.m[3], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (ST)
+#pragma unroll
+    for (int r = FEAT_KSTEPS; r < 16; ++r)
+      buf_store4(st, vo, r * 1024, E->m[r / 4][4 * (r % 4)], E->m[r / 4][4 * (r % 4) + 1], E->m[r / 4][4 * (r % 4) + 2],
+                 E->m[r / 4][4 * (r % 4) + 3]);
+}
+__device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const float4* __restrict__ Wf) {
+  feat_gemm_st<false>(acc, x, Wf, nullptr, make_rsrc(Wf));
 }
 
 // One 32-edge block `blk` of task `task` (receivers g0 .. g0+31): for LAYER >= 1 the edge
@@ -587,9 +618,13 @@ __device__ __forceinline__ int32_t edge_sender(const MpnnArgs& a, int64_t g0, in
 #endif
 }
 
+#ifndef E_STORE_SPREAD
+#define E_STORE_SPREAD 1
+#endif
 template <int LAYER>
 __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int64_t g0, int lane, int blk,
-                                           int32_t s_pre, Tile& m, const float4* w1_lds = nullptr) {
+                                           int32_t s_pre, Tile& m, const float4* w1_lds = nullptr,
+                                           uint64_t* stp = nullptr) {
   const int te = 32 * blk + (lane & 31);
   const int rl = te / 50;
   const int64_t g = g0 + rl;
@@ -634,8 +669,9 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
     tile_layer_norm(e, a.edge_ln_s, a.edge_ln_o);
 #endif
   }
+  STAMP(0);
 #ifndef PST_EXP_NOSTORE
-  if (a.e_out) tile_store_blk(e, a.e_out + eblk);
+  if (a.e_out && !E_STORE_SPREAD) tile_store_blk(e, a.e_out + eblk);
 #endif
   // message MLP of layer LAYER
   if (LAYER == 0) {
@@ -644,13 +680,26 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
     // features: 16 k-steps instead of 64
     tile_add_rows(m, a.PM0 + (int64_t)ls0 * 256 + 0, a.PM0 + (int64_t)lr0 * 256 + 128);
     tile_add_row(m, a.Utab + (int64_t)(ls0 - lr0 + 511) * 128);
-    feat_gemm(m, x, a.W_msg0f);
+#ifndef PST_EXP_NOSTORE
+    if (E_STORE_SPREAD)  // e leaves during this GEMM, after the gathers above (tile_gemm_store)
+      feat_gemm_st<true>(m, x, a.W_msg0f, &e, make_rsrc_or_null(a.e_out ? a.e_out + eblk : nullptr));
+    else
+#endif
+      feat_gemm(m, x, a.W_msg0f);
+    STAMP(1);
     msg_hidden<w1_lds_ksteps<LAYER>()>(m, a.msg, w1_lds);
   } else {
     tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
-    tile_gemm(m, e, a.msg.w0);
+#ifndef PST_EXP_NOSTORE
+    if (E_STORE_SPREAD)  // e leaves during the GEMM that reads it (tile_gemm_store)
+      tile_gemm_store(m, e, a.msg.w0, make_rsrc_or_null(a.e_out ? a.e_out + eblk : nullptr));
+    else
+#endif
+      tile_gemm(m, e, a.msg.w0);
+    STAMP(1);
     msg_hidden<w1_lds_ksteps<LAYER>()>(m, a.msg, w1_lds);
   }
+  STAMP(2);
 }
 
 // Node update of the 32 receivers g0 .. g0+31 (lane&31 = receiver): x = h + agg/50, where
@@ -744,12 +793,16 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   float* aggl = a.agg + task * 32 * 128;
   float carry[2] = {0.f, 0.f};  // running sums of the receiver continuing into the next block
 
+  uint64_t stp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef PST_STAMP
+  stp[7] = __builtin_amdgcn_s_memtime();
+#endif
   int32_t s_next = edge_sender(a, g0, lane, blk_lo);
   for (int blk = blk_lo; blk < blk_hi; ++blk) {
     const int32_t s_cur = s_next;
     if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
-    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m, w1_lds);
+    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m, w1_lds, stp);
     // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order). The
     // block holds edges of two receivers: rA (block edges 0..lastA) and rA+1 (the rest).
     // Transpose through LDS two accumulator blocks at a time, so that lane l owns channel
@@ -802,6 +855,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
         carry[p] = accA;
       }
     }
+    STAMP(3);
   }
   // the sums were stored by other lanes of this wave (HALF: and by the partner wave): drain
   // stores, then read back
@@ -865,6 +919,13 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
       tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
     }
   }
+  STAMP(4);
+#ifdef PST_STAMP
+  if (lane == 0) {
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_stamps[LAYER][i], (unsigned long long)stp[i]);
+    atomicAdd(&g_stamps[LAYER][5], 1ull);
+  }
+#endif
 }
 
 // Split layer (small batches, where one wave per 32 receivers cannot fill the GPU): the edge
@@ -1805,3 +1866,14 @@ void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float
 }
 
 }  // namespace pst
+
+#ifdef PST_STAMP
+extern "C" int pst_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pst::g_stamps), sizeof(pst::g_stamps)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[3][8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(pst::g_stamps), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
