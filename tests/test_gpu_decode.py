@@ -68,10 +68,11 @@ def _wide_cases():
 
 
 # wide cases (up to 512 residues): float32 noise grows with the protein — the upsampler and IPA
-# softmaxes run over up to 512 keys and the 8 fold iterations compound the frame updates
-# (measured on MI355X, round 2: single ≤ 6.8e-6, pair ≤ 1.9e-5 rel, traj / atoms max ≤ 7.2e-3 Å
-# at 512 residues, 4.7e-4 Å at 128)
-TOL_WIDE = {"single": 2e-5, "pair_rel": 5e-5, "traj": 2e-2, "atoms": 2e-2, "atoms_rms": 3e-3}
+# softmaxes run over up to 512 keys and the 8 fold iterations compound the frame updates.
+# Measured on MI355X (round 3, profiles/r03_decode_wide.txt): single <= 6.9e-6, pair <= 1.9e-5
+# rel; traj / atoms max 4.7e-4 Å (t128, 128 residues), 2.0e-3 (t512), 4.0e-3 (df2, 512 residues),
+# 7.2e-3 Å (df4, 512 residues); atoms rms <= 1.1e-3 Å. Bounds ~1.4x the largest.
+TOL_WIDE = {"single": 1e-5, "pair_rel": 3e-5, "traj": 1e-2, "atoms": 1e-2, "atoms_rms": 1.5e-3}
 
 
 @pytest.mark.parametrize("case", _wide_cases())
