@@ -27,7 +27,8 @@ namespace pst {
 // Diagnostic build only (-DPST_STAMP): per-phase wave cycles of the fused k_mpnn, summed over
 // waves (s_memtime deltas; pst_debug_stamps reads them). Not in the product build.
 #ifdef PST_STAMP
-__device__ unsigned long long g_stamps[3][8];
+__device__ unsigned long long g_stamps[3][16];
+__device__ unsigned long long g_waves[3][16384][4];  // per task: start, end (s_memrealtime), HW_ID | XCC_ID << 32
 #define STAMP(i)                                                        \
   if (stp) {                                                            \
     __builtin_amdgcn_sched_barrier(0);                                  \
@@ -38,6 +39,30 @@ __device__ unsigned long long g_stamps[3][8];
   }
 #else
 #define STAMP(i) (void)stp
+#endif
+
+#ifdef PST_STAMP
+#define STAMP_FLUSH() \
+  if (lane == 0) { \
+    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime(), mt1 = __builtin_amdgcn_s_memtime(); \
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_stamps[LAYER][i], (unsigned long long)stp[i]); \
+    atomicAdd(&g_stamps[LAYER][5], 1ull); \
+    atomicAdd(&g_stamps[LAYER][6], (unsigned long long)stp[6]); \
+    atomicAdd(&g_stamps[LAYER][8], (unsigned long long)(rt1 - st_rt0)); \
+    atomicAdd(&g_stamps[LAYER][9], (unsigned long long)(mt1 - st_mt0)); \
+    atomicMin(&g_stamps[LAYER][10], (unsigned long long)st_rt0); \
+    atomicMax(&g_stamps[LAYER][11], (unsigned long long)rt1); \
+    const int64_t slot = HALF ? 2 * task + hh : task; \
+    if (slot < 16384) { \
+      g_waves[LAYER][slot][0] = st_rt0; \
+      g_waves[LAYER][slot][1] = rt1; \
+      g_waves[LAYER][slot][2] = (uint64_t)__builtin_amdgcn_s_getreg(0xf804) | \
+                                ((uint64_t)__builtin_amdgcn_s_getreg(0xf814) << 32); \
+      g_waves[LAYER][slot][3] = (uint64_t)blockIdx.x; \
+    } \
+  }
+#else
+#define STAMP_FLUSH()
 #endif
 
 #ifndef MPNN_MIN_BLOCKS
@@ -764,6 +789,9 @@ __device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, 
 template <int LAYER, bool HALF>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   __shared__ float lds_scratch[4][64 * 36];
+#ifdef PST_STAMP
+  const uint64_t st_rt0 = __builtin_amdgcn_s_memrealtime(), st_mt0 = __builtin_amdgcn_s_memtime();
+#endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (no waterfalls)
 #ifdef PST_XCD_REMAP
@@ -775,6 +803,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 #else
   const int64_t task = HALF ? (int64_t)blockIdx.x * 2 + (w >> 1) : (int64_t)blockIdx.x * 4 + w;
 #endif
+  const int hh = w & 1;  // HALF: which half of the task's edge blocks
   // the first KL k-steps of the message MLP's W1 fragments (msg_hidden), read by every block of
   // the workgroup's four waves from LDS instead of L2; filled before any wave may leave
   constexpr int KL = w1_lds_ksteps<LAYER>();
@@ -787,7 +816,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   // HALF grids hold exactly n_tasks / 2 workgroups (n_tasks is a multiple of 4): no wave may
   // leave before the barrier below
   if (!HALF && task >= a.n_tasks) return;
-  const int blk_lo = HALF ? 25 * (w & 1) : 0, blk_hi = HALF ? blk_lo + 25 : 50;
+  const int blk_lo = HALF ? 25 * hh : 0, blk_hi = HALF ? blk_lo + 25 : 50;
   const int64_t g0 = task * 32;
   float* scratch = lds_scratch[w];
   float* aggl = a.agg + task * 32 * 128;
@@ -796,6 +825,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   uint64_t stp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef PST_STAMP
   stp[7] = __builtin_amdgcn_s_memtime();
+  stp[6] = stp[7] - st_mt0;  // prologue: W1 staging, first sender
 #endif
   int32_t s_next = edge_sender(a, g0, lane, blk_lo);
   for (int blk = blk_lo; blk < blk_hi; ++blk) {
@@ -866,7 +896,9 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // the node update on both waves of the pair, two output blocks each, tiles exchanged
     // through this pair's half of lds_scratch (free after the edge phase)
-    node_update_pair<LAYER>(a, g0, w & 1, lds_scratch[w & 2]);
+    node_update_pair<LAYER>(a, g0, hh, lds_scratch[w & 2]);
+    STAMP(4);
+    STAMP_FLUSH();
     return;
   } else {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -920,12 +952,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     }
   }
   STAMP(4);
-#ifdef PST_STAMP
-  if (lane == 0) {
-    for (int i = 0; i < 5; ++i) atomicAdd(&g_stamps[LAYER][i], (unsigned long long)stp[i]);
-    atomicAdd(&g_stamps[LAYER][5], 1ull);
-  }
-#endif
+  STAMP_FLUSH();
 }
 
 // Split layer (small batches, where one wave per 32 receivers cannot fill the GPU): the edge
@@ -1868,10 +1895,14 @@ void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float
 }  // namespace pst
 
 #ifdef PST_STAMP
+extern "C" int pst_debug_waves(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pst::g_waves), sizeof(pst::g_waves)) == hipSuccess ? 0 : -1;
+}
 extern "C" int pst_debug_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pst::g_stamps), sizeof(pst::g_stamps)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[3][8] = {};
+    unsigned long long z[3][16] = {};
+    for (int L = 0; L < 3; ++L) z[L][10] = ~0ull;
     if (hipMemcpyToSymbol(HIP_SYMBOL(pst::g_stamps), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

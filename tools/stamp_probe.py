@@ -30,19 +30,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--proteins", type=int, default=512)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--waves", default="", help="save per-task (start, end, HW_ID|XCC_ID<<32, block) here (.npy)")
     a = ap.parse_args()
     samples = synthetic.synthetic_batch(a.proteins, 256, seed=1000)
     pos, flags, off = pack_samples(samples)
     tk = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
     lib = ctypes.CDLL(LIB_PATH)
     lib.pst_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 24)()
+    buf = (ctypes.c_ulonglong * 48)()
     for _ in range(a.reps):
         lib.pst_debug_stamps(buf, 1)
         tk.tokenize_packed(pos.astype(np.float32), flags, off)
         tk.sync()
     lib.pst_debug_stamps(buf, 0)
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(3, 8).astype(np.float64)
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(3, 16).astype(np.float64)
     out = {"proteins": a.proteins, "lib": LIB_PATH, "layers": {}}
     for L in range(3):
         waves = st[L, 5]
@@ -55,7 +56,19 @@ def main():
         tot = sum(st[L, :5]) / waves
         ph["total_cycles_per_task"] = round(tot)
         ph["waves"] = int(waves)
+        ph["prologue_cycles_per_task"] = round(st[L, 6] / waves)
+        span_us = (st[L, 11] - st[L, 10]) / 100.0  # s_memrealtime: 100 MHz
+        ph["kernel_span_us"] = round(span_us, 1)
+        ph["clock_ghz"] = round(st[L, 9] / st[L, 8] * 0.1, 3)
+        # share of the span x 2 048 wave slots (2 per SIMD) that waves occupied
+        ph["slot_occupancy"] = round(st[L, 8] / 100.0 / (span_us * 2048), 3)
+        ph["stamped_share_of_wave_life"] = round(sum(st[L, :5]) / st[L, 9], 3)
         out["layers"][f"k_mpnn<{L}>"] = ph
+    if a.waves:
+        lib.pst_debug_waves.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+        wb = (ctypes.c_ulonglong * (3 * 16384 * 4))()
+        lib.pst_debug_waves(wb)
+        np.save(a.waves, np.frombuffer(wb, dtype=np.uint64).reshape(3, 16384, 4))
     print(json.dumps(out))
 
 
