@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -33,7 +34,10 @@
 namespace pst {
 namespace dec {
 
-enum { F_RELU_OUT = 1, F_RELU_IN = 2, F_ACCUM = 4, F_SIGMOID_OUT = 8 };
+// F_QSCALE: output × key_dim^-0.5 (the upsampler's query scaling, modules.py:346) in the epilogue,
+// the same multiply the separate k_scale pass did
+enum { F_RELU_OUT = 1, F_RELU_IN = 2, F_ACCUM = 4, F_SIGMOID_OUT = 8, F_QSCALE = 16 };
+#define Q_SCALE 0.176776695296637f
 
 __global__ void k_scale(float* x, int64_t n, float s) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -96,6 +100,7 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ X, int l
       if (b) v = v + b[col];
       if (flags & F_RELU_OUT) v = v > 0.0f ? v : 0.0f;
       if (flags & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
+      if (flags & F_QSCALE) v = v * Q_SCALE;
       float* y = Y + (int64_t)r * ldy + col;
       *y = (flags & F_ACCUM) ? *y + v : v;
     }
@@ -195,6 +200,7 @@ __global__ __launch_bounds__(64 * SLICES) void k_gemm_mfma(const float* __restri
       if (b) v = v + b[c];
       if (flags & F_RELU_OUT) v = v > 0.0f ? v : 0.0f;
       if (flags & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
+      if (flags & F_QSCALE) v = v * Q_SCALE;
       float* y = Y + (int64_t)row * ldy + c;
       *y = (flags & F_ACCUM) ? *y + v : v;
     }
@@ -529,10 +535,8 @@ __global__ void k_affine_init(float* __restrict__ aff, float* __restrict__ rot, 
 }
 
 // QuatAffine.pre_compose (quat_affine.py:288-317): q += q ⊗ (0, v); t += R·dt; renormalise
-__global__ void k_affine_update(float* __restrict__ aff, float* __restrict__ rot, const float* __restrict__ upd,
-                                int N) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
+__device__ __forceinline__ void affine_update(float* __restrict__ aff, float* __restrict__ rot,
+                                              const float* __restrict__ upd, int i) {
   float* a = aff + i * 7;
   float* R = rot + i * 9;
   const float* u = upd + i * 6;
@@ -919,12 +923,13 @@ __global__ void k_ipa_local(const float* __restrict__ vpt, const float* __restri
 
 // Backbone torsions → frames → atom14 → atom37 (folding.py:674-746, all_atom.py:473-595, :122-135)
 // plus the trajectory row (affine × [1,1,1,1,10,10,10]).
-__global__ void k_sc_geom(const float* __restrict__ aff, const float* __restrict__ rot,
+__global__ void k_sc_geom(float* __restrict__ aff, float* __restrict__ rot, const float* __restrict__ upd /*[N][6]*/,
                           const float* __restrict__ unnorm /*[N][6]*/, float* __restrict__ angles /*[N][3][2]*/,
                           float* __restrict__ traj /*[N][7]*/, float* __restrict__ atom37 /*[N][37][3] or null*/,
                           float* __restrict__ atom14 /*[N][14][3] or null*/, int N) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
+  affine_update(aff, rot, upd, i);  // this iteration's backbone update first (was k_affine_update)
   const float* a = aff + i * 7;
   const float* R = rot + i * 9;
   float sn[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {1.f, 1.f, 1.f, 1.f};
@@ -1046,6 +1051,10 @@ struct pst_decoder {
   size_t ws_bytes = 0;
   // last call's intermediates (per protein offsets) for pst_decoder_debug
   std::vector<float> last_single, last_pair, last_traj, last_angles, last_atom14;
+  // pinned staging of a group's index arrays (one H2D copy per group) and the event of its copy
+  char* h_up = nullptr;
+  size_t h_up_bytes = 0;
+  hipEvent_t up_ev = nullptr;
   // decode_group's kernel sequence as HIP graphs, keyed by the group's shape (decode_group)
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
 };
@@ -1283,12 +1292,6 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   hipStream_t st = dec->stream;
   const int64_t T = G.T, N = G.N, NP = G.NP;
   t_mfma = !getenv("PST_DECODE_NO_MFMA");
-  DCHK(hipMemcpyAsync(S.tokens, G.tokens.data(), sizeof(uint32_t) * T, hipMemcpyHostToDevice, st));
-  DCHK(hipMemcpyAsync(S.tok_off, G.tok_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
-  DCHK(hipMemcpyAsync(S.node_off, G.node_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
-  DCHK(hipMemcpyAsync(S.pair_off, G.pair_off.data(), sizeof(int64_t) * (G.B + 1), hipMemcpyHostToDevice, st));
-  DCHK(hipMemcpyAsync(S.tok_prot, G.tok_prot.data(), sizeof(int32_t) * T, hipMemcpyHostToDevice, st));
-  DCHK(hipMemcpyAsync(S.node_prot, G.node_prot.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, st));
   std::vector<int32_t> vt_prot, vt_q0;
   for (int b = 0; b < G.B; ++b)
     for (int64_t q0 = 0; q0 < G.node_off[b + 1] - G.node_off[b]; q0 += 16) {
@@ -1296,8 +1299,45 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
       vt_q0.push_back((int32_t)q0);
     }
   const int n_vt = (int)vt_prot.size();
-  DCHK(hipMemcpyAsync(S.vt_prot, vt_prot.data(), sizeof(int32_t) * n_vt, hipMemcpyHostToDevice, st));
-  DCHK(hipMemcpyAsync(S.vt_q0, vt_q0.data(), sizeof(int32_t) * n_vt, hipMemcpyHostToDevice, st));
+  {
+    // The group's index arrays travel as ONE copy from a pinned staging buffer: they are laid out
+    // back to back from the start of the workspace's index region (tok_off ... vt_q0, allocated
+    // consecutively with room for kNodeCap entries each, so the packed form always fits), and the
+    // S pointers are set to that layout (a function of the group's shape, so the graph cache key
+    // still covers every kernel argument). Eight pageable copies cost ~10 us each before.
+    char* const d0 = reinterpret_cast<char*>(S.tok_off);
+    const struct {
+      void** dst;
+      const void* src;
+      size_t bytes;
+    } parts[] = {{(void**)&S.tok_off, G.tok_off.data(), sizeof(int64_t) * (G.B + 1)},
+                 {(void**)&S.node_off, G.node_off.data(), sizeof(int64_t) * (G.B + 1)},
+                 {(void**)&S.pair_off, G.pair_off.data(), sizeof(int64_t) * (G.B + 1)},
+                 {(void**)&S.tok_prot, G.tok_prot.data(), sizeof(int32_t) * T},
+                 {(void**)&S.node_prot, G.node_prot.data(), sizeof(int32_t) * N},
+                 {(void**)&S.tokens, G.tokens.data(), sizeof(uint32_t) * T},
+                 {(void**)&S.vt_prot, vt_prot.data(), sizeof(int32_t) * n_vt},
+                 {(void**)&S.vt_q0, vt_q0.data(), sizeof(int32_t) * n_vt}};
+    size_t total = 0;
+    for (const auto& q : parts) total += (q.bytes + 255) / 256 * 256;
+    if (dec->up_ev) DCHK(hipEventSynchronize(dec->up_ev));  // the previous group's copy has left the buffer
+    if (total > dec->h_up_bytes) {
+      if (dec->h_up) DCHK(hipHostFree(dec->h_up));
+      dec->h_up = nullptr;
+      dec->h_up_bytes = 0;
+      DCHK(hipHostMalloc((void**)&dec->h_up, total));
+      dec->h_up_bytes = total;
+    }
+    size_t off = 0;
+    for (const auto& q : parts) {
+      *q.dst = d0 + off;
+      if (q.bytes) std::memcpy(dec->h_up + off, q.src, q.bytes);
+      off += (q.bytes + 255) / 256 * 256;
+    }
+    DCHK(hipMemcpyAsync(d0, dec->h_up, total, hipMemcpyHostToDevice, st));
+    if (!dec->up_ev) DCHK(hipEventCreateWithFlags(&dec->up_ev, hipEventDisableTiming));
+    DCHK(hipEventRecord(dec->up_ev, st));
+  }
   DecBatch bt{G.B, S.tok_off, S.node_off, S.pair_off, S.tok_prot, S.node_prot};
   const int Ni = (int)N;
   const bool fused = !getenv("PST_DECODE_UNFUSED");
@@ -1311,13 +1351,10 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     for (int b = 0; b < 3; ++b) {
       layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.qn[b]);
       layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.dn[b]);
-      gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, Ni, 0);
+      gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, Ni, F_QSCALE);  // q · key_dim^-0.5
       gemm_raw(st, S.ln_a, 128, W.wg[b], 128, 128, W.gb[b], S.gate, 128, Ni, F_SIGMOID_OUT);
       gemm_raw(st, S.ln_b, 128, W.wk[b], 128, 128, nullptr, S.k, 128, (int)T, 0);
       gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, (int)T, 0);
-      // q · key_dim^-0.5 (modules.py:346)
-      hipLaunchKernelGGL(k_scale, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.q, N * 128,
-                         0.176776695296637f);
       hipLaunchKernelGGL(k_up_attn, dim3((unsigned)N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, bt, N);
       gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, Ni, F_ACCUM);
       layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.rt_ln[b]);
@@ -1390,11 +1427,12 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
       gemm(st, S.tmp384a, 384, W.tr[1], S.tmp384b, 384, Ni, F_RELU_OUT);
       gemm(st, S.tmp384b, 384, W.tr[2], S.act, 384, Ni, F_ACCUM);  // += input_act
       layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.tr_ln);
+      // the affine update (pre_compose with S.upd) runs at the head of k_sc_geom: nothing between
+      // here and there reads the frames
       gemm(st, S.act, 384, W.affine_update, S.upd, 6, Ni, 0);
-      hipLaunchKernelGGL(k_affine_update, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.upd, Ni);
-      // MultiRigidSidechain: (0 + Lin(relu(act))) + Lin(relu(initial_act)), 2 residual blocks, angles
-      hipLaunchKernelGGL(k_zero, dim3((unsigned)((N * 128 + 255) / 256)), dim3(256), 0, st, S.sca, N * 128);
-      gemm(st, S.act, 384, W.sc_in, S.sca, 128, Ni, F_RELU_IN | F_ACCUM);
+      // MultiRigidSidechain: (0 + Lin(relu(act))) + Lin(relu(initial_act)), 2 residual blocks, angles;
+      // the first GEMM writes instead of accumulating onto zeros (0 + v == v up to the sign of a zero)
+      gemm(st, S.act, 384, W.sc_in, S.sca, 128, Ni, F_RELU_IN);
       gemm(st, S.init_relu, 128, W.sc_in1, S.sca, 128, Ni, F_ACCUM);
       // scb is only ever read through a ReLU: apply it in the producing GEMM's epilogue instead of
       // as a copy before the consumer (same values)
@@ -1404,7 +1442,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
       gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, Ni, F_ACCUM);
       gemm(st, S.sca, 128, W.angles, S.unnorm, 6, Ni, F_RELU_IN);
       const bool last = it == 7;
-      hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.unnorm,
+      hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.upd, S.unnorm,
                          S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7, last ? S.atom37 : nullptr,
                          last ? S.atom14 : nullptr, Ni);
     }
@@ -1654,6 +1692,8 @@ int pst_decoder_destroy(pst_decoder* dec) {
     if (p) (void)hipFree(p);
   for (auto& kv : dec->graphs) (void)hipGraphExecDestroy(kv.second);
   dec->graphs.clear();
+  if (dec->h_up) (void)hipHostFree(dec->h_up);
+  if (dec->up_ev) (void)hipEventDestroy(dec->up_ev);
   if (dec->stream) (void)hipStreamDestroy(dec->stream);
   delete dec;
   return PST_OK;

@@ -49,7 +49,14 @@ def _run(cmd, **kw):
 @pytest.mark.parametrize("kind,n_files", [("asan", 31), ("tsan", 6)])
 def test_parser_pool_writer_under_sanitizer(tmp_path, casp14_files, kind, n_files):
     _run(["make", "-s", "-C", CSRC, kind])
-    r = _run([os.path.join(SAN, f"pdb_harness_{kind}"), str(tmp_path)] + casp14_files[:n_files])
+    cmd = [os.path.join(SAN, f"pdb_harness_{kind}"), str(tmp_path)] + casp14_files[:n_files]
+    if kind == "tsan":
+        # TSan refuses to start when the kernel places a mapping outside its shadow layout (high
+        # ASLR entropy on some hosts): that is the runtime failing to start, not a finding
+        probe = subprocess.run(cmd[:1] + [str(tmp_path / "probe")], capture_output=True, text=True, timeout=60)
+        if "ThreadSanitizer: unexpected memory mapping" in probe.stderr:
+            pytest.skip("TSan runtime cannot start on this host (unexpected memory mapping)")
+    r = _run(cmd)
     assert "0 check failures" in r.stdout, r.stdout
 
 
