@@ -124,7 +124,21 @@ __global__ __launch_bounds__(64 * SLICES) void k_gemm_mfma(const float* __restri
                                                            int ldy, int M, int N, int K, int flags, int kslice) {
   __shared__ float part[SLICES][16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int row0 = blockIdx.y * 32, col0 = blockIdx.x * 32 * NACC;
+  // 1-D grid of ncol x nrow tiles. Workgroups are dispatched round-robin over the 8 XCDs (bid % 8),
+  // each with its own L2: when nrow % 8 == 0, XCD x takes row tiles x, x + 8, ... with all their
+  // column tiles, so each 32-row slab of X is fetched into one L2 instead of all eight (the
+  // out_proj GEMM's X is 17 MB at 8 x 256 residues).
+  const int ncol = (N + 32 * NACC - 1) / (32 * NACC), nrow = (M + 31) / 32;
+  int tr, tc;
+  if ((nrow & 7) == 0) {
+    const int x = blockIdx.x & 7, idx = blockIdx.x >> 3;
+    tr = x + 8 * (idx / ncol);
+    tc = idx % ncol;
+  } else {
+    tr = blockIdx.x / ncol;
+    tc = blockIdx.x % ncol;
+  }
+  const int row0 = tr * 32, col0 = tc * 32 * NACC;
   const int i = lane & 31, h = lane >> 5;
   const float* xr = X + (int64_t)min(row0 + i, M - 1) * ldx;  // rows past M: clamped, not stored
   bool cv[NACC];
@@ -1183,7 +1197,7 @@ inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, i
       // slice width rounded UP (to whole 4-k fragment groups): ks · slices >= K, so no tail of K is
       // dropped; the last slices may be short or empty (k1 = min(K, k0 + ks) in the kernel)
       const int ks = ((K + slices - 1) / slices + 3) / 4 * 4;
-      dim3 grid((unsigned)((N + 31) / 32), (unsigned)((M + 31) / 32));
+      const dim3 grid((unsigned)(((N + 31) / 32) * ((M + 31) / 32)));  // 1-D, XCD-aware in the kernel
       hipLaunchKernelGGL(kern, grid, dim3(64 * slices), 0, st, X, ldx, Wt, N, b, Y, ldy, M, N, K, flags, ks);
     };
     if (K >= 1024)
