@@ -161,6 +161,25 @@ def test_grouped_decode_matches_single():
     dec.close()
 
 
+def test_multi_group_decode_matches_single():
+    """A call that spans several decode groups (5 x 512 residues: the pair capacity 2^20 takes 4,
+    the fifth opens a second group) reuses the pinned index staging buffer and the graph cache
+    across groups of different shapes; every protein equals its own single decode."""
+    from pst_amd._native import Decoder
+    rng = np.random.default_rng(29)
+    toks = [rng.integers(0, 4096, 512) for _ in range(5)]
+    toks[4] = toks[4][:300]  # the second group has its own shape
+    dec = Decoder(0, 4096, 1, P.pack_decoder(P.random_full_params(6, 4), 6))
+    together = dec.decode(toks)
+    again = dec.decode(toks)  # graph replay of both group shapes
+    for t, a, want_tok in zip(together, again, toks):
+        assert t.shape[0] == len(want_tok)
+        assert np.array_equal(t, a)
+        alone = dec.decode([want_tok])[0]
+        assert np.max(np.abs(t - alone)) < 1e-3
+    dec.close()
+
+
 def test_token_ids_beyond_codebook_wrap_like_reference():
     """indexes_to_codes (quantize.py:70-79) extracts digits as (id // basis) mod L, so an id >= K
     decodes as id mod K; the decoder accepts such ids instead of rejecting them."""

@@ -93,24 +93,30 @@ __device__ float run_t(int iters) {
 
 // the same wave interleaving its MFMAs with independent VALU work: KIND 0 = 2 v_pk_fma_f32 per
 // MFMA, 1 = 4 v_fma_f32 per MFMA, 2 = one s_nop 0 per MFMA, 3 = one v_rcp_f32 per MFMA
-template <int KIND>
+template <int KIND, int NP = 2, int NS = 4>
 __device__ float run_mix(int iters) {
   f32x16 a0 = {}, a1 = {}, a2 = {}, a3 = {};
   float x = 1e-3f * (threadIdx.x & 63), y = 1.0001f;
-  f32x2 v0 = {x, y}, v1 = {y, x};
-  float s0 = x, s1 = y, s2 = x + y, s3 = x * y;
+  f32x2 v0 = {x, y}, v1 = {y, x}, v2 = {x, x}, v3 = {y, y};
+  float s0 = x, s1 = y, s2 = x + y, s3 = x * y, s4 = x - y, s5 = 2 * x, s6 = 2 * y, s7 = x + 1;
   const f32x2 m = {0.9999f, 0.9998f}, c = {1e-4f, 2e-4f};
   const float ms = 0.9999f, cs = 1e-4f;
 #define MIX_STEP(acc, A, B, SR)                                                                   \
   acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A, B, acc, 0, 0, 0);                              \
   if (KIND == 0) {                                                                              \
-    asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(v0) : "v"(m), "v"(c));                   \
-    asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(v1) : "v"(m), "v"(c));                   \
+    if (NP > 0) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(v0) : "v"(m), "v"(c));       \
+    if (NP > 1) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(v1) : "v"(m), "v"(c));       \
+    if (NP > 2) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(v2) : "v"(m), "v"(c));       \
+    if (NP > 3) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(v3) : "v"(m), "v"(c));       \
   } else if (KIND == 1) {                                                                       \
-    asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s0) : "v"(ms), "v"(cs));                     \
-    asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s1) : "v"(ms), "v"(cs));                     \
-    asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s2) : "v"(ms), "v"(cs));                     \
-    asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s3) : "v"(ms), "v"(cs));                     \
+    if (NS > 0) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s0) : "v"(ms), "v"(cs));         \
+    if (NS > 1) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s1) : "v"(ms), "v"(cs));         \
+    if (NS > 2) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s2) : "v"(ms), "v"(cs));         \
+    if (NS > 3) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s3) : "v"(ms), "v"(cs));         \
+    if (NS > 4) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s4) : "v"(ms), "v"(cs));         \
+    if (NS > 5) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s5) : "v"(ms), "v"(cs));         \
+    if (NS > 6) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s6) : "v"(ms), "v"(cs));         \
+    if (NS > 7) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(s7) : "v"(ms), "v"(cs));         \
   } else if (KIND == 2) {                                                                       \
     asm volatile("s_nop 0");                                                                    \
   } else {                                                                                      \
@@ -126,7 +132,7 @@ __device__ float run_mix(int iters) {
       MIX_STEP(a3, y, y, s3)
     }
   }
-  float s = v0.x + v0.y + v1.x + v1.y + s0 + s1 + s2 + s3;
+  float s = v0.x + v0.y + v1.x + v1.y + v2.x + v2.y + v3.x + v3.y + s0 + s1 + s2 + s3 + s4 + s5 + s6 + s7;
   for (int r = 0; r < 16; ++r) s += a0[r] + a1[r] + a2[r] + a3[r];
   return s;
 }
@@ -146,6 +152,11 @@ __global__ __launch_bounds__(512, 1) void k(float* out, int ra, int rb, int im, 
   else if (role == 7) s = run_mix<1>(im);
   else if (role == 8) s = run_mix<2>(im);
   else if (role == 9) s = run_mix<3>(im);
+  else if (role == 10) s = run_mix<0, 1>(im);
+  else if (role == 11) s = run_mix<0, 4>(im);
+  else if (role == 12) s = run_mix<1, 2, 1>(im);
+  else if (role == 13) s = run_mix<1, 2, 2>(im);
+  else if (role == 14) s = run_mix<1, 2, 8>(im);
   out[blockIdx.x * 512 + threadIdx.x] = s;
 }
 
@@ -156,8 +167,8 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   const int im = 2000, is = 8000, ip = 8000;
-  const char* nm = "_MSPNTabcd";
-  const int pairs[][2] = {{1, 0}, {2, 0}, {3, 0}, {4, 0}, {5, 0}, {1, 1}, {2, 2}, {3, 3}, {4, 4}, {5, 5}, {1, 2}, {1, 3}, {1, 4}, {1, 5}, {2, 3}, {6, 0}, {7, 0}, {8, 0}, {9, 0}, {6, 6}, {7, 7}, {8, 8}, {9, 9}};
+  const char* nm = "_MSPNTabcdefghi";
+  const int pairs[][2] = {{1, 0}, {2, 0}, {3, 0}, {4, 0}, {5, 0}, {1, 1}, {2, 2}, {3, 3}, {4, 4}, {5, 5}, {1, 2}, {1, 3}, {1, 4}, {1, 5}, {2, 3}, {6, 0}, {7, 0}, {8, 0}, {9, 0}, {6, 6}, {7, 7}, {8, 8}, {9, 9}, {10, 10}, {11, 11}, {12, 12}, {13, 13}, {14, 14}};
   for (auto& p : pairs) {
     float best = 1e9f;
     for (int rep = 0; rep < 4; ++rep) {
@@ -171,6 +182,6 @@ int main() {
     }
     printf("%c+%c: %.3f ms\n", nm[p[0]], nm[p[1]], best);
   }
-  printf("per iteration: M = 16 MFMA 32x32x2 f32 (1024 cyc at 64/MFMA), S = 64 v_fma_f32, P = 32 v_pk_fma_f32, N = P + s_nop 0 after each, T = 64 v_rcp_f32; a/b/c/d = M with 2 v_pk_fma / 4 v_fma / 1 s_nop / 1 v_rcp after each MFMA in the same wave\n");
+  printf("per iteration: M = 16 MFMA 32x32x2 f32 (1024 cyc at 64/MFMA), S = 64 v_fma_f32, P = 32 v_pk_fma_f32, N = P + s_nop 0 after each, T = 64 v_rcp_f32; a/b/c/d = M with 2 v_pk_fma / 4 v_fma / 1 s_nop / 1 v_rcp after each MFMA in the same wave; e/f = 1 / 4 v_pk_fma, g/h/i = 1 / 2 / 8 v_fma_f32 after each MFMA\n");
   return 0;
 }
