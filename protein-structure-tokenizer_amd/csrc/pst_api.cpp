@@ -272,6 +272,13 @@ struct pst_ctx {
   bool timing = false;
   hipEvent_t ev[PST_N_STAGES + 1] = {};
   int64_t dbg_cap = 0;
+  // clock probe (measurement only, pst_clock_probe_start/stop): one wave on probe_stream
+  hipStream_t probe_stream = nullptr;
+  unsigned long long* d_probe = nullptr;  // [max][2] (s_memtime, s_memrealtime)
+  int* d_probe_count = nullptr;
+  int* h_probe_stop = nullptr;  // pinned, mapped: the host raises it, the probe wave polls it
+  int32_t probe_cap = 0;
+  bool probe_running = false;
 };
 
 namespace {
@@ -775,6 +782,42 @@ int pst_get_timing(pst_ctx* ctx, float* ms) {
   return PST_OK;
 }
 
+int pst_clock_probe_start(pst_ctx* ctx, int32_t max_samples, int32_t sleep_units) {
+  if (!ctx || max_samples < 2 || sleep_units < 1 || ctx->probe_running) return PST_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->probe_stream) {
+    HIPCHK(hipStreamCreateWithFlags(&ctx->probe_stream, hipStreamNonBlocking));
+    HIPCHK(hipHostMalloc((void**)&ctx->h_probe_stop, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipMalloc((void**)&ctx->d_probe_count, sizeof(int)));
+  }
+  if (max_samples > ctx->probe_cap) {
+    if (ctx->d_probe) HIPCHK(hipFree(ctx->d_probe));
+    HIPCHK(hipMalloc((void**)&ctx->d_probe, sizeof(unsigned long long) * 2 * (size_t)max_samples));
+    ctx->probe_cap = max_samples;
+  }
+  __atomic_store_n(ctx->h_probe_stop, 0, __ATOMIC_SEQ_CST);
+  int* d_stop = nullptr;
+  HIPCHK(hipHostGetDevicePointer((void**)&d_stop, ctx->h_probe_stop, 0));
+  pst::launch_clock_probe(ctx->d_probe, ctx->d_probe_count, max_samples, sleep_units, d_stop, ctx->probe_stream);
+  HIPCHK(hipGetLastError());
+  ctx->probe_running = true;
+  return PST_OK;
+}
+
+int pst_clock_probe_stop(pst_ctx* ctx, uint64_t* samples, int32_t max_samples, int32_t* n_samples) {
+  if (!ctx || !ctx->probe_running || !samples || !n_samples) return PST_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  __atomic_store_n(ctx->h_probe_stop, 1, __ATOMIC_SEQ_CST);
+  HIPCHK(hipStreamSynchronize(ctx->probe_stream));
+  ctx->probe_running = false;
+  int n = 0;
+  HIPCHK(hipMemcpy(&n, ctx->d_probe_count, sizeof(int), hipMemcpyDeviceToHost));
+  n = std::min(n, std::min<int32_t>(max_samples, ctx->probe_cap));
+  if (n > 0) HIPCHK(hipMemcpy(samples, ctx->d_probe, sizeof(unsigned long long) * 2 * (size_t)n, hipMemcpyDeviceToHost));
+  *n_samples = n;
+  return PST_OK;
+}
+
 size_t pst_param_count(int32_t n_levels) {
   HostParams P;
   return walk(nullptr, n_levels, &P);
@@ -873,6 +916,14 @@ int pst_destroy(pst_ctx* ctx) {
   for (hipEvent_t e : ctx->range_ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->idle_ev) (void)hipEventDestroy(ctx->idle_ev);
+  if (ctx->probe_stream) {
+    if (ctx->h_probe_stop) __atomic_store_n(ctx->h_probe_stop, 1, __ATOMIC_SEQ_CST);
+    (void)hipStreamSynchronize(ctx->probe_stream);
+    (void)hipStreamDestroy(ctx->probe_stream);
+  }
+  if (ctx->d_probe) (void)hipFree(ctx->d_probe);
+  if (ctx->d_probe_count) (void)hipFree(ctx->d_probe_count);
+  if (ctx->h_probe_stop) (void)hipHostFree(ctx->h_probe_stop);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return PST_OK;

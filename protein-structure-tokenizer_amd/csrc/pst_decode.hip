@@ -655,11 +655,6 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   __syncthreads();
   const float* kT = kT_all + n0;  // column j = key j of this protein
   const float* kpT = kpT_all + n0;
-#ifdef PST_EXP_NO_IPA_LOGITS  // timing-only ablation (results differ): logits = pair bias only
-  for (int j = tid; j < N; j += 256)
-    for (int h = 0; h < 12; ++h) attT[j * ATT_LD + h] = b2d[(int64_t)j * 12 + h];
-  if (false)
-#endif
   for (int j = tid; j < N; j += 256) {
     const float4* brow = reinterpret_cast<const float4*>(b2d + (int64_t)j * 12);
     float bb[12];
@@ -715,11 +710,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
     float* ao = att_out + (bt.pair_off[bprot] + (int64_t)il * N) * 12;
     for (int e = tid; e < N * 12; e += 256) ao[e] = attT[(e / 12) * ATT_LD + e % 12];
   }
-#ifdef PST_EXP_NO_IPA_PAIR  // timing-only ablation (results differ): skip the pair sums
-  if (false)
-#else
   if (MFMA_PAIR)
-#endif
   {
     // pair attention on the matrix cores: lane (i = lane & 15, g = lane >> 4) feeds A = z[4s+g][c0+i]
     // and B = att[head i][4s+g] (0 for the 4 padding heads); after the chain it holds
@@ -793,9 +784,6 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
     float pacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float vacc[2] = {0.f, 0.f};
     int j = 0;
-#ifdef PST_EXP_NO_IPA_VALUES  // timing-only ablation (results differ): skip the value sums
-    if (MFMA_PAIR) j = N;
-#endif
     for (; j + 8 <= N; j += 8) {
       float zv[8], v0[8], v1[8];
 #pragma unroll

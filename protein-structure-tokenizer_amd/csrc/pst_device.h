@@ -527,17 +527,9 @@ struct ActId {
 // GELU of the previous layer's output (its bias is already in the accumulator: chains start
 // from the bias)
 struct ActGelu {
-#if defined(PST_EXP_NOGELU)  // ablation: identity (results differ; timing only)
-  __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return x; }
-#elif defined(PST_SCALAR_GELU)
-  __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return (f32x2){c_gelu(x.x), c_gelu(x.y)}; }
-#elif defined(PST_C_GELU)
-  __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return c_gelu2(x); }
-#else
   __device__ __forceinline__ f32x2 operator()(int t, f32x2 x) const {
     return t < 4 ? c_gelu2_asm<true>(x) : c_gelu2_asm<false>(x);
   }
-#endif
 };
 
 struct ActBiasRelu {

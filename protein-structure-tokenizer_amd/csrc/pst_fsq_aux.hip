@@ -110,32 +110,6 @@ __global__ __launch_bounds__(256) void k_fsq_aux(FsqAuxArgs a) {
   const f32x4* A4 = reinterpret_cast<const f32x4*>(sA);
   const f32x4* E4 = reinterpret_cast<const f32x4*>(sEA);
   const int qlo = a.K_lo >> 2;
-#ifdef PST_AUX_SPLIT
-  // A/B: the distances row first, then the soft_proba row (one write stream per block at a time)
-  if (dist)
-    for (int q = threadIdx.x; q < nq; q += 256) {
-      const int khi = q / qlo;
-      const float bb = sB[khi];
-      f32x4 v = A4[q - khi * qlo];
-      v.x = v.x + bb;
-      v.y = v.y + bb;
-      v.z = v.z + bb;
-      v.w = v.w + bb;
-      __builtin_nontemporal_store(v, dist + q);
-    }
-  if (prob)
-    for (int q = threadIdx.x; q < nq; q += 256) {
-      const int khi = q / qlo;
-      const float eb = sEB[khi];
-      f32x4 v = E4[q - khi * qlo];
-      v.x = (v.x * eb) * inv_s;
-      v.y = (v.y * eb) * inv_s;
-      v.z = (v.z * eb) * inv_s;
-      v.w = (v.w * eb) * inv_s;
-      __builtin_nontemporal_store(v, prob + q);
-    }
-  return;
-#endif
   for (int q = threadIdx.x; q < nq; q += 256) {
     const int khi = q / qlo;
     const int ql = q - khi * qlo;

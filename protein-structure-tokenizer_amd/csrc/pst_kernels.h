@@ -164,4 +164,10 @@ void launch_fsq_aux(const FsqAuxArgs& a, int n_prot, hipStream_t st);
 void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, const float* init, float* Y,
                        int ldy, hipStream_t st);
 
+// Measurement only: one wave stamps (s_memtime, s_memrealtime) into out[2i], out[2i+1] every
+// ~sleep_units x 8 K cycles until *stop (host-mapped) is set or max_samples are taken; *count =
+// samples written. The clock between samples is d(memtime) / d(memrealtime) x 100 MHz.
+void launch_clock_probe(unsigned long long* out, int* count, int max_samples, int sleep_units, const int* stop,
+                        hipStream_t st);
+
 }  // namespace pst

@@ -24,47 +24,6 @@
 
 namespace pst {
 
-// Diagnostic build only (-DPST_STAMP): per-phase wave cycles of the fused k_mpnn, summed over
-// waves (s_memtime deltas; pst_debug_stamps reads them). Not in the product build.
-#ifdef PST_STAMP
-__device__ unsigned long long g_stamps[3][16];
-__device__ unsigned long long g_waves[3][16384][4];  // per task: start, end (s_memrealtime), HW_ID | XCC_ID << 32
-#define STAMP(i)                                                        \
-  if (stp) {                                                            \
-    __builtin_amdgcn_sched_barrier(0);                                  \
-    const uint64_t _t = __builtin_amdgcn_s_memtime();                   \
-    stp[i] += _t - stp[7];                                              \
-    stp[7] = _t;                                                        \
-    __builtin_amdgcn_sched_barrier(0);                                  \
-  }
-#else
-#define STAMP(i) (void)stp
-#endif
-
-#ifdef PST_STAMP
-#define STAMP_FLUSH() \
-  if (lane == 0) { \
-    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime(), mt1 = __builtin_amdgcn_s_memtime(); \
-    for (int i = 0; i < 5; ++i) atomicAdd(&g_stamps[LAYER][i], (unsigned long long)stp[i]); \
-    atomicAdd(&g_stamps[LAYER][5], 1ull); \
-    atomicAdd(&g_stamps[LAYER][6], (unsigned long long)stp[6]); \
-    atomicAdd(&g_stamps[LAYER][8], (unsigned long long)(rt1 - st_rt0)); \
-    atomicAdd(&g_stamps[LAYER][9], (unsigned long long)(mt1 - st_mt0)); \
-    atomicMin(&g_stamps[LAYER][10], (unsigned long long)st_rt0); \
-    atomicMax(&g_stamps[LAYER][11], (unsigned long long)rt1); \
-    const int64_t slot = HALF ? 2 * task + hh : task; \
-    if (slot < 16384) { \
-      g_waves[LAYER][slot][0] = st_rt0; \
-      g_waves[LAYER][slot][1] = rt1; \
-      g_waves[LAYER][slot][2] = (uint64_t)__builtin_amdgcn_s_getreg(0xf804) | \
-                                ((uint64_t)__builtin_amdgcn_s_getreg(0xf814) << 32); \
-      g_waves[LAYER][slot][3] = (uint64_t)blockIdx.x; \
-    } \
-  }
-#else
-#define STAMP_FLUSH()
-#endif
-
 #ifndef MPNN_MIN_BLOCKS
 #define MPNN_MIN_BLOCKS 2
 #endif
@@ -221,53 +180,6 @@ __device__ int rank_select(const double* cen, int64_t base, int n, int rr, int c
   return rr;
 }
 
-#ifdef PST_KNN_ROUNDS
-// one DPP step of a lexicographic (distance, index) argmin: combine with the lane `ctrl` selects
-// (lanes the row mask excludes keep their own pair)
-__device__ __forceinline__ void argmin_dpp_step(double& d, int& s, int ctrl, int row_mask) {
-  const long long bits = __double_as_longlong(d);
-  const int lo = (int)bits, hi = (int)(bits >> 32);
-  int plo, phi, ps;
-  switch (ctrl) {  // the DPP control must be an immediate
-#define PST_DPP_CASE(C, RM)                                            \
-  case C:                                                              \
-    plo = __builtin_amdgcn_update_dpp(lo, lo, C, RM, 0xf, false);      \
-    phi = __builtin_amdgcn_update_dpp(hi, hi, C, RM, 0xf, false);      \
-    ps = __builtin_amdgcn_update_dpp(s, s, C, RM, 0xf, false);         \
-    break;
-    PST_DPP_CASE(0xB1, 0xf)
-    PST_DPP_CASE(0x4E, 0xf)
-    PST_DPP_CASE(0x141, 0xf)
-    PST_DPP_CASE(0x140, 0xf)
-    PST_DPP_CASE(0x142, 0xa)
-    PST_DPP_CASE(0x143, 0xc)
-#undef PST_DPP_CASE
-    default:
-      plo = lo; phi = hi; ps = s;
-  }
-  (void)row_mask;
-  const double pd = __longlong_as_double(((long long)phi << 32) | (unsigned)plo);
-  if (lex_less(pd, ps, d, s)) {
-    d = pd;
-    s = ps;
-  }
-}
-
-// wave-wide lexicographic argmin: quad xor 1, 2, half-row mirror, row mirror, row broadcasts;
-// the result lands in lane 63 and is read back as a uniform value
-__device__ __forceinline__ void wave_argmin(double& d, int& s) {
-  argmin_dpp_step(d, s, 0xB1, 0xf);
-  argmin_dpp_step(d, s, 0x4E, 0xf);
-  argmin_dpp_step(d, s, 0x141, 0xf);
-  argmin_dpp_step(d, s, 0x140, 0xf);
-  argmin_dpp_step(d, s, 0x142, 0xa);
-  argmin_dpp_step(d, s, 0x143, 0xc);
-  const long long bits = __double_as_longlong(d);
-  const int lo = __builtin_amdgcn_readlane((int)bits, 63), hi = __builtin_amdgcn_readlane((int)(bits >> 32), 63);
-  s = __builtin_amdgcn_readlane(s, 63);
-  d = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-#endif
 
 // LDS of k_knn's radix select, one slice per wave
 __shared__ unsigned knn_hist[4][256];
@@ -310,7 +222,6 @@ __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
   const int drop = n <= KNN ? 0 : 1;  // column 0 (self) dropped when n > k (protein_utils.py:385-389)
   int my_s = -1;
   double my_d = 0.0;
-#ifndef PST_KNN_ROUNDS
   {
     // Radix select of the keep smallest (distance, index) pairs: 8 passes of an 8-bit histogram
     // over the distance bits (non-negative doubles order like their bit patterns) find the exact
@@ -415,31 +326,13 @@ __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
       my_d = sd[lane + drop];
     }
   }
-#else
-  unsigned taken = 0;
-  for (int t = 0; t < keep; ++t) {
-    double bd = __builtin_inf();
-    int bs = 0x7fffffff;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      int s = lane + 64 * i;
-      bool ok = s < n && !((taken >> i) & 1u);
-      if (ok && lex_less(d[i], s, bd, bs)) { bd = d[i]; bs = s; }
-    }
-    wave_argmin(bd, bs);  // DPP row ops, no LDS round trips (6 % faster than __shfl_xor)
-    if ((bs & 63) == lane) taken |= 1u << (bs >> 6);
-    if (t - drop == lane) { my_s = bs; my_d = bd; }
-  }
-#endif
   const int deg = n <= KNN ? n : KNN;
   if (lane == 0) a.deg[g] = deg;
   if (lane < KNN) {
     if (n >= KNN) {
       snd[lane] = (int32_t)(base + my_s);
-#ifndef PST_EXP_KNN_NOFEAT
       edge_features(a.frame + g * 9, a.frame + (base + my_s) * 9, a.ca + g * 3, a.ca + (base + my_s) * 3, my_d,
                     feat + lane * 32);
-#endif
     } else {
       // n < k (preprocessing.py:229-260): senders stay per-row, features keep the n*n order
       snd[lane] = lane < n ? (int32_t)(base + my_s) : (int32_t)g;
@@ -490,9 +383,6 @@ __device__ __forceinline__ void tile_add_rows(Tile& acc, const float* __restrict
   for (int M = 0; M < 4; ++M)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#ifdef PST_STREAM_ADD
-      __builtin_amdgcn_sched_barrier(0);
-#endif
       float4 v = p[M * 4 + q];
       acc.m[M][4 * q + 0] = acc.m[M][4 * q + 0] + v.x;
       acc.m[M][4 * q + 1] = acc.m[M][4 * q + 1] + v.y;
@@ -635,12 +525,7 @@ __device__ __forceinline__ void feat_gemm(Tile& acc, const float (&x)[16], const
 // projection rows), so fetching it during the previous block's GEMMs takes one memory latency
 // off every block.
 __device__ __forceinline__ int32_t edge_sender(const MpnnArgs& a, int64_t g0, int lane, int blk) {
-#ifdef PST_EXP_HOT_GATHER
-  const int te = 32 * blk + (lane & 31);
-  return (int32_t)(g0 + te / 50);
-#else
   return a.senders[g0 * KNN + 32 * blk + (lane & 31)];
-#endif
 }
 
 #ifndef E_STORE_SPREAD
@@ -648,18 +533,13 @@ __device__ __forceinline__ int32_t edge_sender(const MpnnArgs& a, int64_t g0, in
 #endif
 template <int LAYER>
 __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int64_t g0, int lane, int blk,
-                                           int32_t s_pre, Tile& m, const float4* w1_lds = nullptr,
-                                           uint64_t* stp = nullptr) {
+                                           int32_t s_pre, Tile& m, const float4* w1_lds = nullptr) {
   const int te = 32 * blk + (lane & 31);
   const int rl = te / 50;
   const int64_t g = g0 + rl;
   const int64_t E = g * KNN + (te - 50 * rl);
   const int64_t s = s_pre;
-#ifdef PST_EXP_HOTE
-  const int64_t eblk = (task * 50) * 4096;
-#else
   const int64_t eblk = (task * 50 + blk) * 4096;
-#endif
   Tile e;
   float x[16];  // layer 0: this lane's edge features
   int lr0 = 0, ls0 = 0;
@@ -690,14 +570,9 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
     mlp3(acc, ein, a.edge);
     tile_load_blk(e, a.e_in + eblk);
     tile_add(e, acc);
-#ifndef PST_EXP_NOLN
     tile_layer_norm(e, a.edge_ln_s, a.edge_ln_o);
-#endif
   }
-  STAMP(0);
-#ifndef PST_EXP_NOSTORE
   if (a.e_out && !E_STORE_SPREAD) tile_store_blk(e, a.e_out + eblk);
-#endif
   // message MLP of layer LAYER
   if (LAYER == 0) {
     // first layer through the embedding's factors: e0·W = T[s-r]·W + f·(Wf·W),
@@ -705,26 +580,19 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
     // features: 16 k-steps instead of 64
     tile_add_rows(m, a.PM0 + (int64_t)ls0 * 256 + 0, a.PM0 + (int64_t)lr0 * 256 + 128);
     tile_add_row(m, a.Utab + (int64_t)(ls0 - lr0 + 511) * 128);
-#ifndef PST_EXP_NOSTORE
     if (E_STORE_SPREAD)  // e leaves during this GEMM, after the gathers above (tile_gemm_store)
       feat_gemm_st<true>(m, x, a.W_msg0f, &e, make_rsrc_or_null(a.e_out ? a.e_out + eblk : nullptr));
     else
-#endif
       feat_gemm(m, x, a.W_msg0f);
-    STAMP(1);
     msg_hidden<w1_lds_ksteps<LAYER>()>(m, a.msg, w1_lds);
   } else {
     tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
-#ifndef PST_EXP_NOSTORE
     if (E_STORE_SPREAD)  // e leaves during the GEMM that reads it (tile_gemm_store)
       tile_gemm_store(m, e, a.msg.w0, make_rsrc_or_null(a.e_out ? a.e_out + eblk : nullptr));
     else
-#endif
       tile_gemm(m, e, a.msg.w0);
-    STAMP(1);
     msg_hidden<w1_lds_ksteps<LAYER>()>(m, a.msg, w1_lds);
   }
-  STAMP(2);
 }
 
 // Node update of the 32 receivers g0 .. g0+31 (lane&31 = receiver): x = h + agg/50, where
@@ -789,20 +657,9 @@ __device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, 
 template <int LAYER, bool HALF>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   __shared__ float lds_scratch[4][64 * 36];
-#ifdef PST_STAMP
-  const uint64_t st_rt0 = __builtin_amdgcn_s_memrealtime(), st_mt0 = __builtin_amdgcn_s_memtime();
-#endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (no waterfalls)
-#ifdef PST_XCD_REMAP
-  // blocks sharing an XCD (same blockIdx % 8) take a contiguous range of tasks, so the two
-  // workgroups of a protein (and its sender rows) share one L2 (bijective for any grid size)
-  const int nwg = gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = blockIdx.x % 8;
-  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (int)(blockIdx.x / 8);
-  const int64_t task = (int64_t)wg * 4 + w;
-#else
   const int64_t task = HALF ? (int64_t)blockIdx.x * 2 + (w >> 1) : (int64_t)blockIdx.x * 4 + w;
-#endif
   const int hh = w & 1;  // HALF: which half of the task's edge blocks
   // the first KL k-steps of the message MLP's W1 fragments (msg_hidden), read by every block of
   // the workgroup's four waves from LDS instead of L2; filled before any wave may leave
@@ -822,17 +679,12 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   float* aggl = a.agg + task * 32 * 128;
   float carry[2] = {0.f, 0.f};  // running sums of the receiver continuing into the next block
 
-  uint64_t stp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#ifdef PST_STAMP
-  stp[7] = __builtin_amdgcn_s_memtime();
-  stp[6] = stp[7] - st_mt0;  // prologue: W1 staging, first sender
-#endif
   int32_t s_next = edge_sender(a, g0, lane, blk_lo);
   for (int blk = blk_lo; blk < blk_hi; ++blk) {
     const int32_t s_cur = s_next;
     if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
-    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m, w1_lds, stp);
+    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m, w1_lds);
     // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order). The
     // block holds edges of two receivers: rA (block edges 0..lastA) and rA+1 (the rest).
     // Transpose through LDS two accumulator blocks at a time, so that lane l owns channel
@@ -849,10 +701,6 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     const int hiA = min(min(lastA, 31), degA - 1 - j0);  // chain A sums edges [0, hiA]
     const int loB = lastA + 1;                           // chain B sums edges [loB, hiB]
     const int hiB = min(31, lastA + degB);
-#ifdef PST_EXP_NOAGG
-    if (blk == 49) for (int M = 0; M < 4; ++M) aggl[M] = m.m[M][0] + m.m[M][15];
-    continue;
-#endif
     // wave-uniform edge masks of the two chains (bit ee set = edge ee enters the chain)
     const uint32_t mA = (uint32_t)__builtin_amdgcn_readfirstlane(
         hiA < 0 ? 0u : (hiA >= 31 ? 0xffffffffu : (1u << (hiA + 1)) - 1u));
@@ -885,7 +733,6 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
         carry[p] = accA;
       }
     }
-    STAMP(3);
   }
   // the sums were stored by other lanes of this wave (HALF: and by the partner wave): drain
   // stores, then read back
@@ -897,8 +744,6 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     // the node update on both waves of the pair, two output blocks each, tiles exchanged
     // through this pair's half of lds_scratch (free after the edge phase)
     node_update_pair<LAYER>(a, g0, hh, lds_scratch[w & 2]);
-    STAMP(4);
-    STAMP_FLUSH();
     return;
   } else {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -951,8 +796,6 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
       tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
     }
   }
-  STAMP(4);
-  STAMP_FLUSH();
 }
 
 // Split layer (small batches, where one wave per 32 receivers cannot fill the GPU): the edge
@@ -1892,19 +1735,32 @@ void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float
   hipLaunchKernelGGL(k_table_gemm, dim3((tiles + 3) / 4), dim3(256), 0, st, X, n_rows, Wf, b, init, Y, ldy);
 }
 
+// ---------------------------------------------------------------------------- clock probe
+// (measurement only, pst_clock_probe_start/stop; bench.py reports the shader clock the timed
+// steps ran at). Every exit path is bounded: at most max_samples iterations.
+__global__ __launch_bounds__(64) void k_clock_probe(unsigned long long* out, int* count, int max_samples,
+                                                    int sleep_units, const int* stop) {
+  int i = 0;
+  for (; i < max_samples; ++i) {
+    const unsigned long long c = __builtin_amdgcn_s_memtime();
+    const unsigned long long w = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      out[2 * i] = c;
+      out[2 * i + 1] = w;
+    }
+    if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+      ++i;
+      break;
+    }
+    for (int k = 0; k < sleep_units; ++k) __builtin_amdgcn_s_sleep(127);
+  }
+  if (threadIdx.x == 0) *count = i;
+}
+
+void launch_clock_probe(unsigned long long* out, int* count, int max_samples, int sleep_units, const int* stop,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, st, out, count, max_samples, sleep_units, stop);
+}
+
 }  // namespace pst
 
-#ifdef PST_STAMP
-extern "C" int pst_debug_waves(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pst::g_waves), sizeof(pst::g_waves)) == hipSuccess ? 0 : -1;
-}
-extern "C" int pst_debug_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pst::g_stamps), sizeof(pst::g_stamps)) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[3][16] = {};
-    for (int L = 0; L < 3; ++L) z[L][10] = ~0ull;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(pst::g_stamps), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif

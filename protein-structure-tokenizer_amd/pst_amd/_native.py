@@ -40,7 +40,7 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free", "pst_write_files",
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
            "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_decode_ex", "pst_decoder_debug",
-           "pst_build_graph")
+           "pst_build_graph", "pst_clock_probe_start", "pst_clock_probe_stop")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -88,6 +88,8 @@ def lib():
         L.pst_set_timing.argtypes = [P, ctypes.c_int32]
         L.pst_get_timing.argtypes = [P, P]
         L.pst_device_count.argtypes = [P]
+        L.pst_clock_probe_start.argtypes = [P, ctypes.c_int32, ctypes.c_int32]
+        L.pst_clock_probe_stop.argtypes = [P, P, ctypes.c_int32, P]
         L.pst_pdb_parse_files.argtypes = [P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_parse_strings.argtypes = [P, P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_batch_sizes.argtypes = [P, P, P]
@@ -307,6 +309,19 @@ class Tokenizer:
 
     def sync(self):
         self._check(lib().pst_sync(self._h))
+
+    def clock_probe_start(self, max_samples: int = 65536, sleep_units: int = 4):
+        """Start the shader-clock probe (pst_clock_probe_start): one wave on the context's probe
+        stream, one sample every ~sleep_units x 8 K cycles, until clock_probe_stop."""
+        self._probe_max = int(max_samples)
+        self._check(lib().pst_clock_probe_start(self._h, self._probe_max, int(sleep_units)))
+
+    def clock_probe_stop(self):
+        """Stop the probe -> (memtime, memrealtime) samples, uint64 [n, 2]."""
+        buf = np.zeros((self._probe_max, 2), np.uint64)
+        n = ctypes.c_int32(0)
+        self._check(lib().pst_clock_probe_stop(self._h, _ptr(buf), self._probe_max, ctypes.byref(n)))
+        return buf[:n.value]
 
     def build_graph_packed(self, pos, flags, offsets):
         """Residue graphs of a packed batch (pst_build_graph): senders [R,50] int32 (node index

@@ -169,15 +169,18 @@ class TokenizeFn:
     `devices[i]` (one host thread per device; the C calls release the GIL) and returns a dict
     with "tokens" uint32 [*batch_dims, seq_max_size // df] (padding rows carry the padded-token
     id exactly as the reference's output does) and "n_tokens" int32 [*batch_dims]
-    (= tokens_mask.sum(-1) of the reference graph) and "n_nodes" int32 [*batch_dims] (the graph's
-    n_node: residues with N, CA, C and O). `random_key` is accepted and unused, as in
+    (= tokens_mask.sum(-1) of the reference graph); with `with_n_nodes` (set by AutoEncodeFn, off
+    for the reference-shaped `prepare_tokenize_fn` output) also "n_nodes" int32 [*batch_dims] (the
+    graph's n_node: residues with N, CA, C and O). `random_key` is accepted and unused, as in
     the reference's inference path (no stochastic op when is_training=False).
     """
 
-    def __init__(self, cfg: TokenizerConfig, devices: Sequence[int], emit_aux: bool = False):
+    def __init__(self, cfg: TokenizerConfig, devices: Sequence[int], emit_aux: bool = False,
+                 with_n_nodes: bool = False):
         self.cfg = cfg
         self.devices = list(devices)
         self.emit_aux = emit_aux
+        self.with_n_nodes = with_n_nodes
         self._ctx: Dict[Tuple[int, int], _native.Tokenizer] = {}
         self._pool = _cf.ThreadPoolExecutor(max_workers=max(1, len(self.devices)))
 
@@ -217,8 +220,9 @@ class TokenizeFn:
         res = list(self._pool.map(run, range(n_dev)))
         tokens = np.stack([r[0] for r in res]).reshape(*batched_graph.batch_dims, out_len)
         n_tokens = np.stack([r[1] for r in res]).reshape(*batched_graph.batch_dims)
-        n_nodes = np.stack([np.asarray(r[3], np.int32) for r in res]).reshape(*batched_graph.batch_dims)
-        out = {"tokens": tokens, "n_tokens": n_tokens, "n_nodes": n_nodes}
+        out = {"tokens": tokens, "n_tokens": n_tokens}
+        if self.with_n_nodes:
+            out["n_nodes"] = np.stack([np.asarray(r[3], np.int32) for r in res]).reshape(*batched_graph.batch_dims)
         if self.emit_aux:
             for key in res[0][2]:
                 if key == "histogram":
@@ -536,7 +540,7 @@ class AutoEncodeFn:
     def __init__(self, cfg: TokenizerConfig, devices: Sequence[int]):
         self.cfg = cfg
         self.devices = list(devices)
-        self.tokenize = TokenizeFn(cfg, devices, emit_aux=True)
+        self.tokenize = TokenizeFn(cfg, devices, emit_aux=True, with_n_nodes=True)
         self.decode = DecodeFn(cfg, devices)
 
     def __call__(self, model_params: ReplicatedParams, random_key: Any, batched_graph: ProteinBatch):

@@ -43,14 +43,15 @@ def main(pdbs: List[str], token_save_path: str, backend: str, batch_size_per_dev
     The model is selected by `config_overrides` exactly as the reference composes it
     (`model=gnn/ablation_<K>_df_<df>.yaml`, `data=ablation_df_<df>.yaml`,
     `pst_amd.config.config_from_overrides`); an unrecognised override raises instead of
-    falling back to a default. `config_name` is accepted and, as in the reference, not used
-    (the composed config is always `vq3d_inference`) unless `config_path` points at the
-    reference's YAML tree, which is then composed with Hydra's rules under that name.
+    falling back to a default. `config_name` is accepted and, as in the reference, not used:
+    the composed config is always `vq3d_inference` (`/root/reference/scripts/tokenize_pdb.py:40-45`),
+    also when `config_path` points at the reference's YAML tree, which is then composed with
+    Hydra's rules.
     Keyword-only extras: `weights_dir` (directory of `params.npz`; default the config's
     `weight_paths`) and `config_path`.
     """
     if config_path:
-        cfg = C.config_from_hydra(C.load_config(config_name or "vq3d_inference", job_name="tokenize",
+        cfg = C.config_from_hydra(C.load_config("vq3d_inference", job_name="tokenize",
                                                 overrides=config_overrides, config_path=config_path))
     else:
         cfg = C.config_from_overrides(config_overrides)

@@ -17,16 +17,21 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True)
 def _clear_pipeline_env():
     yield
-    for k in ("PST_H2D_CHUNKS", "PST_H2D_GRAPH_RANGES"):
+    for k in ("PST_H2D_CHUNKS", "PST_H2D_GRAPH_RANGES", "PST_H2D_COPY_STREAMS"):
         os.environ.pop(k, None)
 
 
-def _ctx(chunks, cb=4096, df=1, ranges=None):
-    """ranges: copy ranges of the first chunk (PST_H2D_GRAPH_RANGES; None = the policy). The
-    context reads both variables at its FIRST tokenize call, so they stay set until the test
-    ends (or the next _ctx call replaces them)."""
+def _ctx(chunks, cb=4096, df=1, ranges=None, copy_streams=None):
+    """ranges: copy ranges of the first chunk (PST_H2D_GRAPH_RANGES; None = the policy);
+    copy_streams: PST_H2D_COPY_STREAMS (2 = odd ranges copied on a second stream). The context
+    reads these variables at its FIRST tokenize call, so they stay set until the test ends (or
+    the next _ctx call replaces them)."""
     from pst_amd._native import Tokenizer
     os.environ["PST_H2D_CHUNKS"] = str(chunks)
+    if copy_streams is None:
+        os.environ.pop("PST_H2D_COPY_STREAMS", None)
+    else:
+        os.environ["PST_H2D_COPY_STREAMS"] = str(copy_streams)
     if ranges is None:
         os.environ.pop("PST_H2D_GRAPH_RANGES", None)
     else:
@@ -47,9 +52,11 @@ def test_chunked_h2d_is_bitwise_identical(cb, df):
     # below the default policy's half-round gate, so the default (None) takes one copy and an
     # explicit PST_H2D_GRAPH_RANGES forces the range branch; the plan each call took is checked.
     # (the first chunk of a forced 3- or 8-chunk plan holds only a few proteins, so it gets at
-    # most that many ranges)
-    for chunks, ranges, want_ranges in ((1, 1, 0), (1, None, 0), (1, 4, 4), (1, 8, 8), (3, 4, None), (8, 8, None)):
-        t = _ctx(chunks, cb, df, ranges)
+    # most that many ranges). The last two repeat (1, 4) and (3, 4) with the odd ranges copied on
+    # a second stream (PST_H2D_COPY_STREAMS=2): the range events then come from two streams.
+    for chunks, ranges, want_ranges, cs in ((1, 1, 0, None), (1, None, 0, None), (1, 4, 4, None), (1, 8, 8, None),
+                                            (3, 4, None, None), (8, 8, None, None), (1, 4, 4, 2), (3, 4, None, 2)):
+        t = _ctx(chunks, cb, df, ranges, cs)
         tok, nt, nn = t.tokenize_packed(pos, flags, off)
         plan = t.last_plan_detail()
         assert plan["chunks"] == chunks and len(plan["cuts"]) == chunks + 1, (chunks, ranges, plan)
@@ -155,3 +162,29 @@ def test_two_proteins_small_first():
         assert np.array_equal(o[1], outs[0][1]) and np.array_equal(o[2], outs[0][2])
         assert list(o[2]) == [60, 480]
         assert np.array_equal(o[0], outs[0][0])
+
+
+def test_clock_probe_runs_beside_tokenize_and_stops():
+    """pst_clock_probe_start/stop (bench.py's clock field): the probe wave samples while a
+    tokenize call runs on the context's stream, stops when asked, and the clock it implies is a
+    plausible gfx950 shader clock; a second start while running and a stop without a probe are
+    PST_E_INVALID. The tokens are the same with and without the probe."""
+    from pst_amd._native import PstError, Tokenizer
+    samples = synthetic.synthetic_batch(64, 256, seed=1000)
+    pos, flags, off = pack_samples(samples)
+    t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
+    tok0, _, _ = t.tokenize_packed(pos, flags, off)
+    t.clock_probe_start(max_samples=4096, sleep_units=4)
+    with pytest.raises(PstError):
+        t.clock_probe_start(max_samples=4096, sleep_units=4)
+    tok1, _, _ = t.tokenize_packed(pos, flags, off)
+    s = t.clock_probe_stop()
+    with pytest.raises(PstError):
+        t.clock_probe_stop()
+    t.close()
+    assert np.array_equal(tok0, tok1)
+    assert 3 <= len(s) <= 4096
+    dc = np.diff(s[:, 0].astype(np.float64))
+    dw = np.diff(s[:, 1].astype(np.float64))
+    ghz = dc.sum() / dw.sum() * 0.1
+    assert 0.3 < ghz < 3.0, ghz
