@@ -41,6 +41,7 @@ for _p in (os.path.join(ROOT, "tests", "golden"), ROOT, os.path.join(ROOT, "prot
 
 N_PROT, N_RES, CODEBOOK, DF = 1024, 256, 4096, 1
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (and packed-f32 VALU) peak
+SPEC_GHZ = 2.4             # the shader clock the peak is quoted at
 H, K = 128, 50
 MFMA_FLOP = 32 * 32 * 2 * 2  # one v_mfma_f32_32x32x2_f32
 # MFMA instructions per 32-receiver task (equal to the PMC SQ_INSTS_MFMA per launch
@@ -96,7 +97,8 @@ def parse():
                     help="time pst_tokenize on float64 positions instead of pst_tokenize_f32 on float32 ones")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the CASP14 end-to-end field")
-    ap.add_argument("--cpu-sample", type=int, default=8, help="proteins in the reference-as-computed CPU sample")
+    ap.add_argument("--cpu-sample", type=int, default=64,
+                    help="proteins in the reference-as-computed CPU sample (spread over the workload)")
     ap.add_argument("--port-sample", type=int, default=128, help="proteins in the C-port CPU sample")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_k_mpnn1.json"),
                     help="PMC-measured HBM bytes per residue of k_mpnn<1> (tools/pmc_traffic.sh)")
@@ -194,33 +196,47 @@ def plan_only(args, rank, world):
         dist.destroy_process_group()
 
 
-def reference_exact_match(args, ids, tok, off, plan=None):
-    """Token ids of the fixture proteins this rank holds vs the reference's float64 forward
-    (forward_ref_wide.npz: bench256_p0..7 at 4096/df 1, bench512_p0..1 at 64000/df 4), with the
-    rounding-margin report (tests/golden/refwide.py)."""
+def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
+    """Token ids of the fixture proteins this rank holds vs the reference's own forward
+    (Vq3D.encode_and_quantize under the shim, float64 with JAX's float32 PE argument, i.e. the
+    reference's PE values): the headline workload's exact-match sample, every 8th protein
+    (forward_ref_bench.npz, 128 proteins, make_forward_bench.py), plus the proteins of
+    forward_ref_wide.npz the workload holds (bench256 p0-7, 200, 511, 777, 1023; bench512 p0-1 at
+    64000/df 4). With `bounded` (our FSQ-bounded latents, pst_aux) the report carries our
+    deviation from the reference's latent and its ratio to the rounding margin (refwide.report)."""
     try:
         import refwide
         F = refwide.load()
     except Exception:
         return None
+    try:
+        FB = refwide.load_bench() if (args.codebook, args.df, args.residues) == (4096, 1, 256) else None
+    except Exception:
+        FB = None
     tag = {(4096, 1, 256): "bench256_p{}_k4096_df1", (64000, 4, 512): "bench512_p{}_k64000_df4"}.get(
         (args.codebook, args.df, args.residues))
     if tag is None:
         return None
-    reps, prots = [], []
+    reps, prots, src = [], [], {}
     for i, p in enumerate(ids):
-        c = tag.format(p)
-        if c + "/tokens" not in F.files:
+        if FB is not None and f"bench256_p{p}/tokens_pe32" in FB.files:
+            c, G, want = f"bench256_p{p}", FB, None
+        elif tag.format(p) + "/tokens" in F.files:
+            c, G = tag.format(p), F
+            want = F[c + "/tokens"]
+        else:
             continue
-        T = int(F[c + "/meta"][1])
+        T = int(G[c + "/meta"][1])
         got = tok[off[i]:off[i] + T]
-        want = F[c + "/tokens"]
-        bref = F[c + "/bounded_pe32"] if c + "/bounded_pe32" in F.files else F[c + "/bounded"]
-        tref = F[c + "/tokens_pe32"] if c + "/tokens_pe32" in F.files else want
-        r = refwide.report(bref, tref, bref, got)  # deviation not known here: margins only
-        r["identical_to_f64_reference"] = int(np.sum(got == want))
+        bref = G[c + "/bounded_pe32"] if c + "/bounded_pe32" in G.files else G[c + "/bounded"]
+        tref = G[c + "/tokens_pe32"] if c + "/tokens_pe32" in G.files else want
+        bours = bounded[off[i]:off[i] + T] if bounded is not None else bref  # no deviation known: margins only
+        r = refwide.report(bref, tref, bours, got)
+        if want is not None:
+            r["identical_to_f64_reference"] = int(np.sum(got == want))
         reps.append(r)
         prots.append(p)
+        src[p] = "forward_ref_bench" if G is FB else "forward_ref_wide"
     if not reps:
         return None
     r = refwide.merge(reps)
@@ -229,13 +245,48 @@ def reference_exact_match(args, ids, tok, off, plan=None):
     if cuts:
         pos_of = {p: i for i, p in enumerate(ids)}
         chunk_of = {p: int(np.searchsorted(cuts, pos_of[p], side="right") - 1) for p in prots}
-    return {"proteins": prots, "pipeline_chunk_of_protein": chunk_of,
+    by_chunk = {}
+    for p, rep in zip(prots, reps):
+        k = str(chunk_of.get(p, 0))
+        b = by_chunk.setdefault(k, {"proteins": 0, "tokens": 0, "identical": 0})
+        b["proteins"] += 1
+        b["tokens"] += rep["tokens"]
+        b["identical"] += rep["identical"]
+    return {"proteins_compared": len(prots), "proteins_from_bench_fixture": sum(v == "forward_ref_bench" for v in src.values()),
             "tokens_compared": r["tokens"], "identical": r["identical"], "rate": r["rate"],
-            "identical_to_f64_reference": int(sum(x["identical_to_f64_reference"] for x in reps)),
-            "min_margin": r["min_margin"], "margin_histogram_all": r["margin_histogram_all"],
+            "by_pipeline_chunk": by_chunk,
+            "identical_to_f64_reference": int(sum(x.get("identical_to_f64_reference", 0) for x in reps)),
+            "f64_reference_tokens_compared": int(sum(x["tokens"] for x in reps if "identical_to_f64_reference" in x)),
+            "min_margin": r["min_margin"],
+            "max_deviation": r["max_deviation"] if bounded is not None else None,
+            "max_deviation_over_margin": r["max_deviation_over_margin"] if bounded is not None else None,
+            "mismatches_explained_by_rounding": r["mismatches_explained_by_rounding"],
+            "margin_histogram_all": r["margin_histogram_all"],
             "margin_histogram_mismatches": r["margin_histogram_mismatches"],
             "against": "reference Vq3D.encode_and_quantize run in float64 under the shim with JAX's float32 "
-                       "PE argument (tests/golden/forward_ref_wide.npz, make_forward_wide.py)"}
+                       "PE argument (tests/golden/forward_ref_bench.npz: every 8th protein of the workload, "
+                       "make_forward_bench.py; tests/golden/forward_ref_wide.npz, make_forward_wide.py)"}
+
+
+def clock_stats(samples, window_ms=1.0):
+    """Shader clock from the probe's (s_memtime, s_memrealtime @ 100 MHz) stamps: the mean over the
+    probed span (total cycles / total time) and the slowest `window_ms` window."""
+    if samples is None or len(samples) < 3:
+        return None
+    s = samples.astype(np.float64)
+    dc, dw = np.diff(s[:, 0]), np.diff(s[:, 1])
+    ok = dw > 0
+    dc, dw = dc[ok], dw[ok]
+    mean = float(dc.sum() / dw.sum() * 0.1)
+    t = np.cumsum(dw) / 1e5  # ms
+    win = np.floor(t / window_ms).astype(np.int64)
+    wc = np.bincount(win, weights=dc)
+    ww = np.bincount(win, weights=dw)
+    full = ww >= 0.5 * window_ms * 1e5
+    per = wc[full] / ww[full] * 0.1 if full.any() else np.array([mean])
+    return {"mean_ghz": round(mean, 4), "min_ghz": round(float(per.min()), 4),
+            "p10_ghz": round(float(np.percentile(per, 10)), 4), "p90_ghz": round(float(np.percentile(per, 90)), 4),
+            "span_ms": round(float(t[-1]), 1), "samples": int(len(samples)), "window_ms": window_ms}
 
 
 def casp14_end_to_end(tk):
@@ -247,7 +298,7 @@ def casp14_end_to_end(tk):
     from pst_amd.runner import save_npy_files
     arc = os.path.join(ROOT, "tests", "golden", "casp14_pdbs.tar.gz")
     if not os.path.exists(arc):
-        return None
+        return None, None
     threads = min(16, host_cores())
     # inputs and token files on tmpfs where there is one: the figure is the software path (parse,
     # H2D + tokenize, .npy encode + write syscalls), not the speed of the box's disk
@@ -271,46 +322,79 @@ def casp14_end_to_end(tk):
             if rep:
                 runs.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2))
         R = int(B.offsets[-1])
+        casp = (np.array(B.positions), np.array(B.flags), np.array(B.offsets), (tok.copy(), np.array(nt)))
         tot, parse, tok, write = runs[int(np.argsort([r[0] for r in runs])[len(runs) // 2])]  # median run
         res = {"workload": "CASP14 31 structures (SURVEY config 2), codebook 4096, df 1", "residues": R,
                "parse_ms": round(parse * 1e3, 2), "tokenize_ms": round(tok * 1e3, 2),
                "write_ms": round(write * 1e3, 2), "residues_per_s": round(R / tot, 1),
                "parse_threads": threads, "runs": f"median of {len(runs)} after one warm-up",
                "files_on": shm or tempfile.gettempdir()}
-    return res
+    return res, casp
 
 
-def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=None):
-    """(reference-as-computed torch CPU at all allowed cores and at 8 threads, ragged C port, and
-    the GPU-vs-C-oracle exact match on the port's sample)."""
+def _ref_as_computed_rate(model, pf, df, threads, cores, what):
+    """Time the reference-as-computed PyTorch-CPU forward one protein per call (the reference CLI's
+    batch_size_per_device default), graphs padded as the reference pads them."""
+    import torch
+    from oracle.reference_as_computed import padded_graphs
+    torch.set_num_threads(threads)
+    model.forward(padded_graphs(pf[:1], model.df))  # warm-up
+    res_n = int(sum(p.shape[0] for p, _ in pf))
+    toks = []
+    t0 = time.perf_counter()
+    for i in range(len(pf)):
+        toks.append(model.forward(padded_graphs(pf[i:i + 1], df))["tokens"][0])
+    dt = time.perf_counter() - t0
+    return {"value": round(res_n / dt, 1), "unit": "residues/s", "cores": threads, "kind": "port",
+            "sample": f"{what} ({len(pf)} proteins, {res_n} residues), {dt:.1f} s: the reference's computation as it "
+                      "runs it (graph padded to 512 nodes / 25 600 edges, per-edge PE, dense masked cross-attention, "
+                      "FSQ distances/soft_proba over all K), PyTorch-CPU float32 (oracle/reference_as_computed.py) + "
+                      f"the C graph, one protein per call; torch.set_num_threads({threads}) of {cores} cores available"}, toks
+
+
+def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=None, casp=None):
+    """CPU baselines (reported, not targeted): the reference-as-computed PyTorch-CPU
+    forward on a `--cpu-sample`-protein subset of the workload (every 16th protein by default, so
+    both pipeline chunks) and on SURVEY config 2 (the 31 CASP14 structures, `casp` = (positions,
+    flags, offsets, GPU tokens) from casp14_end_to_end), each at all allowed cores and at 8 threads;
+    the ragged C port; and the GPU-vs-C-oracle exact match on the port's sample."""
     import torch
     from oracle import oracle as O
-    from oracle.reference_as_computed import ReferenceAsComputed, padded_graphs
+    from oracle.reference_as_computed import ReferenceAsComputed
     from pst_amd import params as P
     cores = host_cores()
-    out = {}
-    n = min(args.cpu_sample, len(samples))
     model = ReferenceAsComputed(P.random_params(len(levels), 1234), levels, args.df)
-    pf = [(s.atom37_positions, s.atom_flags()) for s in samples[:n]]
-    res_n = int(sum(s.nb_residues for s in samples[:n]))
+    nb = len(samples)
+    n = min(args.cpu_sample, nb)
+    csel = np.arange(0, nb, max(1, nb // max(1, n)))[:n]
+    pf = [(samples[i].atom37_positions, samples[i].atom_flags()) for i in csel]
+    out = {}
+    ident = None
     for threads in sorted({cores, 8}, reverse=True):
-        log(f"reference-as-computed CPU baseline, {threads} threads, {n} proteins")
-        torch.set_num_threads(threads)
-        model.forward(padded_graphs(pf[:1], args.df))  # warm-up
-        t0 = time.perf_counter()
-        for i in range(n):  # one protein per call (the reference's batch_size_per_device=1 CLI default)
-            model.forward(padded_graphs(pf[i:i + 1], args.df))
-        dt = time.perf_counter() - t0
-        out[threads] = {"value": round(res_n / dt, 1), "unit": "residues/s", "cores": threads, "kind": "port",
-                        "sample": f"first {n} proteins of the workload ({res_n} residues), {dt:.1f} s: the "
-                                  "reference's computation as it runs it (graph padded to 512 nodes / 25 600 "
-                                  "edges, per-edge PE, dense masked cross-attention, FSQ distances/soft_proba "
-                                  "over all K), PyTorch-CPU float32 (oracle/reference_as_computed.py) + the C "
-                                  f"graph; torch.set_num_threads({threads}) of {cores} cores available"}
+        log(f"reference-as-computed CPU baseline (config 3 subset), {threads} threads, {len(pf)} proteins")
+        out[threads], toks = _ref_as_computed_rate(model, pf, args.df, threads, cores,
+                                                   f"every {max(1, nb // max(1, n))}th protein of the workload")
+        if ident is None:
+            ident = sum(int(np.sum(t[:off[i + 1] - off[i]] == gpu_tok[off[i]:off[i + 1]])) for t, i in zip(toks, csel))
+            out[threads]["tokens_identical_to_gpu"] = f"{ident} / {int(sum(off[i + 1] - off[i] for i in csel))}"
+    cfg2 = {}
+    if casp is not None and args.codebook == 4096 and args.df == 1:
+        cpos, cflags, coff, ctok = casp
+        cpf = [(cpos[coff[i]:coff[i + 1]], cflags[coff[i]:coff[i + 1]]) for i in range(len(coff) - 1)]
+        for threads in sorted({cores, 8}, reverse=True):
+            log(f"reference-as-computed CPU baseline (config 2, CASP14), {threads} threads")
+            cfg2[threads], toks = _ref_as_computed_rate(model, cpf, args.df, threads, cores,
+                                                        "SURVEY config 2: the 31 CASP14 structures")
+            if threads == max(cores, 8):
+                eq = tot = 0
+                for i, t in enumerate(toks):
+                    m = int(ctok[1][i])
+                    eq += int(np.sum(t[:m] == ctok[0][coff[i]:coff[i] + m]))
+                    tot += m
+                cfg2[threads]["tokens_identical_to_gpu"] = f"{eq} / {tot}"
     torch.set_num_threads(cores)
     # the C-port sample is spread over the whole workload (every stride-th protein), so it checks
     # every pipeline chunk the timed step runs, not only the first
-    nb = len(samples)
     stride = max(1, -(-nb // max(1, args.port_sample)))
     sel = np.arange(0, nb, stride)
     lens = off[sel + 1] - off[sel]
@@ -340,7 +424,7 @@ def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=No
              "proteins_compared": int(len(sel)), "sample": f"every {stride}th protein",
              "by_pipeline_chunk": by_chunk,
              "against": "C oracle (bitwise canonical path)"}
-    return out[cores], out.get(8), port, exact
+    return out[cores], out.get(8), cfg2.get(cores), cfg2.get(8), port, exact
 
 
 def main():
@@ -396,6 +480,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # shader clock over the timed steps: one probe wave on the context's own side stream
+    # (pst_clock_probe_start/stop), started before and stopped after the bracketed region
+    tk.clock_probe_start(max_samples=1 << 18, sleep_units=4)
     times = []
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -406,6 +493,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    clock = clock_stats(tk.clock_probe_stop())
     plan = tk.last_plan_detail()  # chunks and layer schedule of the timed step (rank 0's share)
     log(f"rank {rank}: {args.steps} timed steps in {elapsed:.2f} s")
     stats = torch.tensor(times + [elapsed], dtype=torch.float64, device=red_dev)
@@ -435,7 +523,7 @@ def main():
                    "note": "rank 0's shard, median of 5 after one warm-up"}
 
     # exact match vs the reference fixtures of the proteins this rank holds (summed over ranks)
-    ref_match = reference_exact_match(args, ids, tok, off, plan)
+    ref_match = reference_exact_match(args, ids, tok, off, plan, bounded=tk.aux(R)["bounded"])
     if world > 1:
         cnt = torch.tensor([ref_match["tokens_compared"], ref_match["identical"]] if ref_match else [0, 0],
                            dtype=torch.float64, device=red_dev)
@@ -464,10 +552,12 @@ def main():
         dts.append(time.perf_counter() - t0)
     tk.set_timing(True)
     stage = None
+    tk.clock_probe_start(max_samples=1 << 16, sleep_units=4)
     for _ in range(3):
         dstep()
         st = tk.stage_ms()
         stage = st if stage is None else {k: stage[k] + st[k] for k in st}
+    stage_clock = clock_stats(tk.clock_probe_stop())
     stage = {k: v / 3 for k, v in stage.items()}
     tk.set_timing(False)
 
@@ -498,6 +588,11 @@ def main():
                 "FLOPs instead, which the kernel's algebraic rewrites (DESIGN.md 5) execute in 0.52x the work",
         "launch_ms": round(dom_ms, 3),
         "effective_alg_tflops": round(MPNN1_ALG_FLOP_PER_RES * R / (dom_ms * 1e-3) / 1e12, 2),
+        # the peak is quoted at the 2.4 GHz spec clock; at the clock the chip actually held over
+        # the stage-timing steps (probe, mean) the reachable peak is peak x clock / 2.4
+        "stage_clock": stage_clock,
+        "frac_at_measured_clock": (round(executed / (PEAK_FP32_TFLOPS * stage_clock["mean_ghz"] / SPEC_GHZ), 4)
+                                   if stage_clock else None),
         "kernels": kern,
         "stage_ms": {k: round(v, 3) for k, v in stage.items()},
         "path_effective_alg_tflops": (round(PATH_ALG_FLOP_PER_RES[args.df] * R / (sum(stage.values()) * 1e-3) / 1e12, 2)
@@ -505,11 +600,12 @@ def main():
     }
 
     log("device-resident rate and stage times done")
-    e2e = casp14_end_to_end(tk) if (rank == 0 and world == 1 and not args.no_e2e) else None
-    cpu = cpu8 = port = exact = None
+    e2e, casp = casp14_end_to_end(tk) if (rank == 0 and world == 1 and not args.no_e2e) else (None, None)
+    cpu = cpu8 = cpu_c2 = cpu_c2_8 = port = exact = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baselines")
-        cpu, cpu8, port, exact = cpu_baselines(args, samples, blob, levels, pos, flags, off, tok, plan)
+        cpu, cpu8, cpu_c2, cpu_c2_8, port, exact = cpu_baselines(args, samples, blob, levels, pos, flags, off, tok,
+                                                                 plan, casp)
 
     if rank == 0:
         mode = "weak" if args.weak else "strong"
@@ -544,11 +640,18 @@ def main():
             "device_resident": {"residues_per_s_per_gpu": round(R / float(np.median(dts)), 1),
                                 "ms": round(float(np.median(dts)) * 1e3, 3),
                                 "note": "rank 0's shard with inputs already in HBM (pst_tokenize_device), median of 5"},
+            "clock": clock,
+            "ms_per_step_at_2p4ghz": (round(med * 1e3 * clock["mean_ghz"] / SPEC_GHZ, 3) if clock else None),
+            "clock_note": ("shader clock over the timed steps (rank 0), one probe wave stamping s_memtime / "
+                           "s_memrealtime on a side stream (pst_clock_probe_start/stop); ms_per_step_at_2p4ghz "
+                           "scales the step as if all of it ran at the clock (the H2D part does not)"),
             "roofline": roofline,
             "exact_match_reference": ref_match,
             "exact_match": exact,
             "cpu_baseline": cpu,
             "cpu_baseline_8_threads": cpu8,
+            "cpu_baseline_config2": cpu_c2,
+            "cpu_baseline_config2_8_threads": cpu_c2_8,
             "cpu_baseline_ragged_port": port,
             "casp14_end_to_end": e2e,
         }

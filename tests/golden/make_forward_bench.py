@@ -1,0 +1,85 @@
+"""Reference-forward fixture for the HEADLINE workload's exact-match sample (build container only).
+
+`bench.py` checks token ids on every 8th protein of `synthetic_batch(1024, 256, seed=1000)`
+(proteins 0, 8, …, 1016: 128 proteins, 32 768 tokens, both pipeline chunks). This script runs the
+REFERENCE's own `Vq3D.encode_and_quantize` (model.py:453-479) under the import shim on each of
+them — the `_pe32` rendering of `make_forward_wide.py` (float64 with the sinusoidal PE argument
+rounded to float32 exactly as JAX forms it with x64 off, i.e. the reference's own PE values) —
+at codebook 4096, df 1, random weights `params.random_params(6, 1234)` (the bench's).
+
+Kept per protein `bench256_p{p}`: the reference's token ids, its FSQ-bounded latents (float64),
+the per-token rounding margin, `meta` = [n, T, codebook, df, D, seed], and the SHA-256 of the
+float32 inputs plus the generator arguments. The inputs themselves are NOT stored: they are
+regenerated from `pst_amd.synthetic.synthetic_protein(256, 1000 + p)` and must hash to the stored
+SHA (`tests/test_fixture_recipes.py`), which keeps the file small and the recipe honest.
+
+    python tests/golden/make_forward_bench.py [--jobs 7] [--stride 8]
+"""
+import argparse
+import os
+import sys
+import time
+from multiprocessing import get_context
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "forward_ref_bench.npz")
+N_PROT, N_RES, SEED0, CODEBOOK, DF = 1024, 256, 1000, 4096, 1
+
+
+def proteins(stride=8):
+    return list(range(0, N_PROT, stride))
+
+
+def case_name(p):
+    return f"bench256_p{p}"
+
+
+def run_one(p):
+    sys.path.insert(0, HERE)
+    import make_forward_wide as M
+    t0 = time.time()
+    name, out = M.run_case((case_name(p), ("syn", N_RES, SEED0 + p), CODEBOOK, DF), pe32=True)
+    pos, fl, sha = M.load_inputs(("syn", N_RES, SEED0 + p))
+    T = len(out["tokens_pe32"])
+    keep = {
+        "tokens_pe32": out["tokens_pe32"],
+        "bounded_pe32": out["bounded_pe32"],
+        "margin_pe32": out["margin_pe32"],
+        "meta": np.array([out["n_nodes"], T, CODEBOOK, DF, out["bounded_pe32"].shape[1], M.PARAM_SEED], np.int64),
+        "input_sha256": np.array(sha),
+        "synthetic_args": np.array([N_RES, SEED0 + p], np.int64),
+    }
+    return p, keep, time.time() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=7)
+    ap.add_argument("--stride", type=int, default=8)
+    args = ap.parse_args()
+    sys.path.insert(0, HERE)
+    import _refenv
+    if not _refenv.available():
+        sys.exit("reference not available")
+    sys.path.insert(0, _refenv.PKG)
+    old = dict(np.load(OUT)) if os.path.exists(OUT) else {}
+    todo = [p for p in proteins(args.stride) if f"{case_name(p)}/tokens_pe32" not in old]
+    print(f"{len(todo)} proteins to run", flush=True)
+    done = 0
+    with get_context("spawn").Pool(args.jobs) as pool:
+        for p, res, dt in pool.imap_unordered(run_one, todo):
+            for k, v in res.items():
+                old[f"{case_name(p)}/{k}"] = v
+            done += 1
+            print(f"p{p}: T={res['meta'][1]} min margin={res['margin_pe32'].min():.3e} ({dt:.0f} s) "
+                  f"[{done}/{len(todo)}]", flush=True)
+            if done % 16 == 0:  # checkpoint: a killed run resumes where it stopped
+                np.savez_compressed(OUT, **old)
+    np.savez_compressed(OUT, **old)
+    print("wrote", OUT)
+
+
+if __name__ == "__main__":
+    main()

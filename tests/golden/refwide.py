@@ -14,12 +14,18 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PATH = os.path.join(HERE, "forward_ref_wide.npz")
+# the headline workload's exact-match sample (every 8th bench protein, make_forward_bench.py)
+BENCH_PATH = os.path.join(HERE, "forward_ref_bench.npz")
 # log10 bins of the margin histogram: [0, 1e-7), [1e-7, 1e-6), ..., [1e-1, 0.5]
 EDGES = [0.0, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2, 1e-1, 0.5000001]
 
 
 def load():
     return np.load(PATH)
+
+
+def load_bench():
+    return np.load(BENCH_PATH)
 
 
 def cases(F, prefix=""):

@@ -39,3 +39,16 @@ def test_casp14_inputs_match_atom37_fixture():
         a, b = int(C["offsets"][i]), int(C["offsets"][i + 1])
         for cb in (4096, 64000):
             assert np.array_equal(F[f"casp_{nm}_k{cb}_df1/in_positions"], C["positions"][a:b])
+
+
+def test_bench_fixture_inputs_reproduce():
+    """forward_ref_bench.npz stores no inputs: every 8th protein of bench.py's workload must
+    regenerate to the SHA-256 the reference forward ran on."""
+    FB = refwide.load_bench()
+    names = refwide.cases(FB)
+    assert names == sorted(f"bench256_p{p}" for p in range(0, 1024, 8))
+    for c in names:
+        n_res, seed = (int(v) for v in FB[c + "/synthetic_args"])
+        assert (n_res, seed) == (256, 1000 + int(c.split("_p")[1]))
+        s = synthetic.synthetic_protein(n_res, seed)
+        assert M.input_sha(s.atom37_positions.astype(np.float32), s.atom_flags()) == str(FB[c + "/input_sha256"]), c

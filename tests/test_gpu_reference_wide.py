@@ -60,3 +60,29 @@ def test_gpu_config4_casp14_k64000():
     assert len(names) == 31
     for c in names:
         assert np.array_equal(out[c][0], F[c + "/tokens"]), c
+
+
+def test_gpu_tokens_equal_reference_bench_sample():
+    """The headline workload's exact-match sample: every 8th protein of bench.py's
+    synthetic_batch(1024, 256, seed=1000) (forward_ref_bench.npz, 128 proteins, 32 768 tokens) in
+    ONE ragged batch through the C ABI, against the reference's forward (_pe32 rendering)."""
+    from pst_amd import synthetic
+    from pst_amd._native import pack_samples
+    FB = refwide.load_bench()
+    names = refwide.cases(FB)
+    samples = [synthetic.synthetic_protein(*(int(v) for v in FB[c + "/synthetic_args"])) for c in names]
+    pos, flags, off = pack_samples(samples)
+    tk = _make(4096, 1, 6, 1234)
+    tok, nt, nn = tk.tokenize_packed(pos.astype(np.float32), flags, off)
+    b = tk.aux(int(off[-1]))["bounded"]
+    tk.close()
+    reps = []
+    for i, c in enumerate(names):
+        n, T = (int(v) for v in FB[c + "/meta"][:2])
+        assert nn[i] == n and nt[i] == T
+        a = int(off[i])
+        assert np.abs(b[a:a + T] - FB[c + "/bounded_pe32"]).max() < TOL["_pe32"][1], c
+        reps.append(refwide.report(FB[c + "/bounded_pe32"], FB[c + "/tokens_pe32"], b[a:a + T], tok[a:a + T]))
+    r = refwide.merge(reps)
+    print({k: r[k] for k in ("tokens", "identical", "min_margin", "max_deviation", "max_deviation_over_margin")})
+    assert r["tokens"] == 32768 and r["identical"] == r["tokens"], r

@@ -103,3 +103,43 @@ def test_reference_as_computed_torch_matches_fixture():
         assert np.array_equal(o["tokens"][0, :T], F[c + "/tokens_pe32"]), c
         assert np.array_equal(o["tokens"][0, :T], F[c + "/tokens_f32"]), c
         assert np.abs(o["bounded"][0, :T] - F[c + "/bounded_pe32"]).max() < 1e-4
+
+
+# ------------------------------------------------------------ the headline workload's sample
+# forward_ref_bench.npz (golden/make_forward_bench.py): the reference's forward (_pe32 rendering)
+# on every 8th protein of bench.py's workload, synthetic_batch(1024, 256, seed=1000) at codebook
+# 4096 / df 1 — the 128 proteins (32 768 tokens) its exact-match sample covers. Inputs are not
+# stored: they regenerate from the generator (SHA-checked in test_fixture_recipes.py).
+FB = refwide.load_bench()
+
+
+def _bench_inputs(c):
+    from pst_amd import synthetic
+    n_res, seed = (int(v) for v in FB[c + "/synthetic_args"])
+    s = synthetic.synthetic_protein(n_res, seed)
+    return s.atom37_positions, s.atom_flags()
+
+
+def test_oracle_tokens_equal_reference_bench_sample():
+    names = refwide.cases(FB)
+    assert len(names) == 128
+
+    def run(c):
+        pos, fl = _bench_inputs(c)
+        return c, O.tokenize(P.random_blob(6, 1234), LEVELS[4096], 1, pos, fl)
+
+    with ThreadPoolExecutor(8) as ex:
+        outs = dict(ex.map(run, names))
+    reps = []
+    for c in names:
+        n, T, cb, df, D, seed = (int(v) for v in FB[c + "/meta"])
+        assert (cb, df, D, seed) == (4096, 1, 6, 1234)
+        out = outs[c]
+        assert out["graph"]["n"] == n and len(out["tokens"]) == T
+        assert np.abs(out["b"] - FB[c + "/bounded_pe32"]).max() < TOL["_pe32"][1], c
+        assert np.array_equal(refwide.dim_margins(FB[c + "/bounded_pe32"]).min(-1), FB[c + "/margin_pe32"])
+        reps.append(refwide.report(FB[c + "/bounded_pe32"], FB[c + "/tokens_pe32"], out["b"], out["tokens"]))
+    r = refwide.merge(reps)
+    print({k: r[k] for k in ("tokens", "identical", "min_margin", "max_deviation", "max_deviation_over_margin")})
+    assert r["tokens"] == 32768
+    assert r["identical"] == r["tokens"], r
