@@ -237,6 +237,10 @@ int pst_pdb_batch_sizes(const pst_pdb_batch* b, int32_t* n, int64_t* n_residues)
  *   aatype [R] u8 (restype index, 20 = UNK), offsets [n+1] i64, status [n] i32 */
 int pst_pdb_batch_copy(const pst_pdb_batch* b, double* positions, uint8_t* flags, uint8_t* aatype,
                        int64_t* offsets, int32_t* status);
+/* The same with positions as float32 [R,37,3]: exact (the parser rounds every coordinate to
+ * float32 as Bio stores atom.coord), half the bytes — the input pst_tokenize_f32 takes. */
+int pst_pdb_batch_copy_f32(const pst_pdb_batch* b, float* positions, uint8_t* flags, uint8_t* aatype,
+                           int64_t* offsets, int32_t* status);
 const char* pst_pdb_batch_error(const pst_pdb_batch* b, int32_t i);
 void pst_pdb_batch_free(pst_pdb_batch* b);
 
@@ -272,7 +276,8 @@ void* pst_stream(pst_ctx* ctx);
  *   which = 20:   int32[20] plan of the last pst_tokenize(_f32) call: [0] copy ranges of its first
  *                 chunk (0 = one copy, the range branch not taken), [1] pipeline chunks C,
  *                 [2 .. 2+C] the chunks' first proteins (and n_prot), [11 .. 11+C-1] each chunk's
- *                 layer schedule (0 fused one wave per task, 1 fused two waves per task, 2 split),
+ *                 layer schedule (0 fused one wave per task, 1 fused two waves per task, 2 split,
+ *                 3 fused as the persistent half-task queue),
  *                 [19] the last chunk's downsampler form (0 one wave per tile, 1 four waves per
  *                 tile, 2 two waves per tile) */
 int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes);

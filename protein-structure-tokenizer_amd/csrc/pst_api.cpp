@@ -35,6 +35,9 @@ constexpr double FUSED_SINGLE_ROUND = 1.1;
 // (use_half_tasks): both wave slots of every SIMD busy, about one round of full-size cost plus
 // the node update on one wave.
 constexpr double FUSED_HALF_ROUND = 1.02;
+// Fused layers of more than one round run as a persistent queue of half tasks (k_mpnn_q): the
+// unit is 25 edge blocks, so a layer's last units are half as long and its tail half as deep.
+constexpr bool MPNN_QUEUE_DEFAULT = true;
 bool use_half_tasks(int64_t n_tasks, int64_t n_simds) { return 2 * n_tasks > n_simds && n_tasks <= n_simds; }
 bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
   const int64_t k = (n_tasks + n_simds - 1) / n_simds;
@@ -226,6 +229,7 @@ struct pst_ctx {
     uint32_t* tokens;
     int32_t* n_tok;
     int64_t* row_start;
+    int32_t* qctr;  // k_mpnn_q's counters, per layer: [8 heads x 16] + [n_tasks]
   } w{};
   // last call's outputs the aux kernels read (device; the caller's buffers for pst_tokenize_device)
   const uint32_t* last_tokens = nullptr;
@@ -246,6 +250,8 @@ struct pst_ctx {
   int32_t* h_counts = nullptr;  // pinned host copy of [n_tok | n_nodes] (cap_B each)
   int32_t last_down_form = 0;  // pst::DOWN_* of the last run (pst_debug_fetch 20, plan[19])
   int64_t half_tasks = -2;   // PST_HALF_TASKS: 1 = fused layers always two waves per task, 0 = never; -1 = policy
+  int64_t mpnn_queue = -2;   // PST_MPNN_QUEUE: 1 = fused layers as the half-task queue (k_mpnn_q) whenever not
+                             // k_mpnn<L, true>, 0 = never (k_mpnn<L, false>); -1 = policy
   std::vector<int64_t> h_offsets;
   // pst_tokenize's H2D pipeline: proteins copied in chunks on copy_stream, chunk k+1's copy
   // overlapping chunk k's compute on `stream` (H2D_MAX_CHUNKS events)
@@ -480,6 +486,7 @@ int ensure_workspace(pst_ctx* ctx, int64_t R, int B) {
       {(void**)&w.pre_proj, sizeof(float) * 128 * Rpad}, {(void**)&w.pos, sizeof(double) * 37 * 3 * Rpad},
       {(void**)&w.flags, sizeof(uint8_t) * 37 * Rpad},  {(void**)&w.tokens, sizeof(uint32_t) * Rpad},
       {(void**)&w.row_start, sizeof(int64_t) * (B + 1)},
+      {(void**)&w.qctr, sizeof(int32_t) * 3 * (128 + Rpad / 32)},
   };
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 4095) / 4096 * 4096;
@@ -622,7 +629,10 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
       split && n_tasks <= (ctx->node_coop >= 0 ? ctx->node_coop : (int64_t)(NODE_COOP_SIMD_FRACTION * ctx->n_simds));
   env_threshold(ctx->half_tasks, "PST_HALF_TASKS");
   const bool half = !split && (ctx->half_tasks >= 0 ? ctx->half_tasks != 0 : use_half_tasks(n_tasks, ctx->n_simds));
-  ctx->last_sched = split ? 2 : half ? 1 : 0;
+  env_threshold(ctx->mpnn_queue, "PST_MPNN_QUEUE");
+  const bool queue = !split && !half && (ctx->mpnn_queue >= 0 ? ctx->mpnn_queue != 0 : MPNN_QUEUE_DEFAULT);
+  ctx->last_sched = split ? 2 : half ? 1 : queue ? 3 : 0;
+  if (queue) HIPCHK(hipMemsetAsync(w.qctr, 0, sizeof(int32_t) * 3 * (128 + n_tasks), st));
   float* msg_rows = nullptr;
   int32_t bpw = 1;
   if (split) {
@@ -652,6 +662,11 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.msg_rows = msg_rows;
     m.blocks_per_wave = bpw;
     m.half_tasks = half ? 1 : 0;
+    if (queue) {
+      m.q_head = w.qctr + l * (128 + n_tasks);
+      m.q_done = m.q_head + 128;
+      m.q_grid = 2 * (ctx->n_simds / 4);  // two 4-wave workgroups per CU (MPNN_MIN_BLOCKS)
+    }
     m.senders = w.senders;
     m.deg = w.deg;
     m.node_local = w.node_local;
@@ -783,7 +798,11 @@ int pst_get_timing(pst_ctx* ctx, float* ms) {
 }
 
 int pst_clock_probe_start(pst_ctx* ctx, int32_t max_samples, int32_t sleep_units) {
-  if (!ctx || max_samples < 2 || sleep_units < 1 || ctx->probe_running) return PST_E_INVALID;
+  if (!ctx) return PST_E_INVALID;
+  if (max_samples < 2 || sleep_units < 1 || ctx->probe_running) {
+    ctx->err = ctx->probe_running ? "clock probe already running" : "clock probe: max_samples >= 2, sleep_units >= 1";
+    return PST_E_INVALID;
+  }
   HIPCHK(hipSetDevice(ctx->device));
   if (!ctx->probe_stream) {
     HIPCHK(hipStreamCreateWithFlags(&ctx->probe_stream, hipStreamNonBlocking));
@@ -805,7 +824,11 @@ int pst_clock_probe_start(pst_ctx* ctx, int32_t max_samples, int32_t sleep_units
 }
 
 int pst_clock_probe_stop(pst_ctx* ctx, uint64_t* samples, int32_t max_samples, int32_t* n_samples) {
-  if (!ctx || !ctx->probe_running || !samples || !n_samples) return PST_E_INVALID;
+  if (!ctx) return PST_E_INVALID;
+  if (!ctx->probe_running || !samples || !n_samples) {
+    ctx->err = ctx->probe_running ? "null argument" : "no clock probe running";
+    return PST_E_INVALID;
+  }
   HIPCHK(hipSetDevice(ctx->device));
   __atomic_store_n(ctx->h_probe_stop, 1, __ATOMIC_SEQ_CST);
   HIPCHK(hipStreamSynchronize(ctx->probe_stream));

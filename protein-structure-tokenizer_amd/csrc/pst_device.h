@@ -375,26 +375,32 @@ __device__ __forceinline__ void tile_store_blk(const Tile& t, float* __restrict_
 // (bias + GELU, bias + ReLU, ...) evaluated just in time, one element per k-step, so its VALU
 // work issues in the shadow of the current k-step's four MFMAs instead of as a separate
 // VALU phase between GEMMs. The schedule interleaves MFMA and VALU groups explicitly.
+// ACT_GROUP k-steps form one scheduling group; the ACT_GROUP/2 activation pairs of the next group
+// are evaluated during the current one (independent chains the scheduler can interleave).
+#ifndef ACT_GROUP
+#define ACT_GROUP 4
+#endif
 template <typename F>
 __device__ __forceinline__ void tile_gemm_f(Tile& acc, const Tile& X, const float4* __restrict__ Wf, F&& f) {
+  constexpr int G = ACT_GROUP, NP = G / 2;
   __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
   const int vo = lane_id() * 16;
   float4 ring[GEMM_DEPTH];
 #pragma unroll
   for (int i = 0; i < GEMM_DEPTH; ++i) ring[i] = buf_load4(rs, vo, i * 1024);
-  // activations run one group of 4 k-steps ahead (two packed pairs per group)
-  f32x2 bq[2], bn[2];
+  // activations run one group of G k-steps ahead (G/2 packed pairs per group)
+  f32x2 bq[NP], bn[NP];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) bq[j] = f(2 * j, (f32x2){X.m[0][2 * j], X.m[0][2 * j + 1]});
+  for (int j = 0; j < NP; ++j) bq[j] = f(2 * j, (f32x2){X.m[0][2 * j], X.m[0][2 * j + 1]});
 #pragma unroll
-  for (int g = 0; g < 16; ++g) {
+  for (int g = 0; g < 64 / G; ++g) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = 4 * g + j;
+    for (int j = 0; j < G; ++j) {
+      const int t = G * g + j;
       float4 a = ring[t % GEMM_DEPTH];
       if (t + GEMM_DEPTH < 64) ring[t % GEMM_DEPTH] = buf_load4(rs, vo, (t + GEMM_DEPTH) * 1024);
-      if (g < 15 && (j & 1) == 0) {
-        const int u = t + 4;
+      if (g < 64 / G - 1 && (j & 1) == 0) {
+        const int u = t + G;
         bn[j >> 1] = f(u, (f32x2){X.m[u / 16][u % 16], X.m[u / 16][u % 16 + 1]});
       }
       const float b = (j & 1) ? bq[j >> 1].y : bq[j >> 1].x;
@@ -404,8 +410,8 @@ __device__ __forceinline__ void tile_gemm_f(Tile& acc, const Tile& X, const floa
       acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b, acc.m[3], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    bq[0] = bn[0];
-    bq[1] = bn[1];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) bq[j] = bn[j];
   }
 }
 
@@ -446,20 +452,21 @@ __device__ __forceinline__ void tile_gemm_store(Tile& acc, const Tile& X, const 
 template <int KL, typename F>
 __device__ __forceinline__ void tile_gemm_mix_f(Tile& acc, const Tile& X, const float4* Wl,
                                                 const float4* __restrict__ Wf, F&& f) {
+  constexpr int G = ACT_GROUP, NP = G / 2;
   __amdgpu_buffer_rsrc_t rs = make_rsrc(Wf);
   const int lane = lane_id();
   const int vo = lane * 16;
   float4 lr[2], ring[GEMM_DEPTH];
   lr[0] = Wl[lane];
   lr[1] = Wl[64 + lane];
-  f32x2 bq[2], bn[2];
+  f32x2 bq[NP], bn[NP];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) bq[j] = f(2 * j, (f32x2){X.m[0][2 * j], X.m[0][2 * j + 1]});
+  for (int j = 0; j < NP; ++j) bq[j] = f(2 * j, (f32x2){X.m[0][2 * j], X.m[0][2 * j + 1]});
 #pragma unroll
-  for (int g = 0; g < 16; ++g) {
+  for (int g = 0; g < 64 / G; ++g) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = 4 * g + j;
+    for (int j = 0; j < G; ++j) {
+      const int t = G * g + j;
       float4 a;
       if (t < KL) {
         a = lr[t % 2];
@@ -473,8 +480,8 @@ __device__ __forceinline__ void tile_gemm_mix_f(Tile& acc, const Tile& X, const 
 #pragma unroll
         for (int i = 0; i < GEMM_DEPTH; ++i) ring[i] = buf_load4(rs, vo, (KL + i) * 1024);
       }
-      if (g < 15 && (j & 1) == 0) {
-        const int u = t + 4;
+      if (g < 64 / G - 1 && (j & 1) == 0) {
+        const int u = t + G;
         bn[j >> 1] = f(u, (f32x2){X.m[u / 16][u % 16], X.m[u / 16][u % 16 + 1]});
       }
       const float b = (j & 1) ? bq[j >> 1].y : bq[j >> 1].x;
@@ -484,8 +491,8 @@ __device__ __forceinline__ void tile_gemm_mix_f(Tile& acc, const Tile& X, const 
       acc.m[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b, acc.m[3], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    bq[0] = bn[0];
-    bq[1] = bn[1];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) bq[j] = bn[j];
   }
 }
 
@@ -528,7 +535,8 @@ struct ActId {
 // from the bias)
 struct ActGelu {
   __device__ __forceinline__ f32x2 operator()(int t, f32x2 x) const {
-    return t < 4 ? c_gelu2_asm<true>(x) : c_gelu2_asm<false>(x);
+    // the first group's pairs are evaluated right after the GEMM that produced them (FRESH)
+    return t < ACT_GROUP ? c_gelu2_asm<true>(x) : c_gelu2_asm<false>(x);
   }
 };
 

@@ -85,6 +85,12 @@ struct MpnnArgs {
   float* msg_rows;
   int32_t blocks_per_wave;  // edge blocks of 32 per k_mpnn_edge wave
   int32_t half_tasks;       // fused mode: two waves per task (k_mpnn<L, true>; n_tasks % 4 == 0)
+  // fused mode as a persistent half-task queue (k_mpnn_q<L>) when non-null: per-XCD queue heads
+  // (8, 64 B apart) and per-task half counters [n_tasks], zeroed before the launch; q_grid =
+  // the workgroups the device holds at once
+  int32_t* q_head;
+  int32_t* q_done;
+  int64_t q_grid;
   // outputs
   float* e_out;  // blocked (null for the last layer)
   float* h_out;

@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include "pst_device.h"
+#include <algorithm>
 #include <utility>
 
 #include "pst_kernels.h"
@@ -647,6 +648,123 @@ __device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t
 template <int LAYER>
 __device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, int h, float* xs);
 
+// The edge phase of one fused-layer task (receivers task*32 .. task*32+31), edge blocks blk_lo ..
+// blk_hi-1 in order: edge update / embedding, message MLP, and the ordered segment sums of the
+// receivers these blocks complete, stored to agg (perm rows). lds_scratch[w]: this wave's LDS tile.
+template <int LAYER>
+__device__ __forceinline__ void mpnn_edge_blocks(const MpnnArgs& a, int64_t task, int lane, int blk_lo, int blk_hi,
+                                                 const float4* w1_lds, float (&lds_scratch)[4][64 * 36], int w) {
+  const int64_t g0 = task * 32;
+  float* scratch = lds_scratch[w];
+  float* aggl = a.agg + task * 32 * 128;
+  float carry[2] = {0.f, 0.f};  // running sums of the receiver continuing into the next block
+
+  int32_t s_next = edge_sender(a, g0, lane, blk_lo);
+  for (int blk = blk_lo; blk < blk_hi; ++blk) {
+    const int32_t s_cur = s_next;
+    if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
+    Tile m;
+    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m, w1_lds);
+    // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order). The
+    // block holds edges of two receivers: rA (block edges 0..lastA) and rA+1 (the rest).
+    // Transpose through LDS two accumulator blocks at a time, so that lane l owns channel
+    // 64·p + l of pass p and runs both receivers' sequential chains over the block's edges
+    // itself. The chain bounds are wave-uniform (no divergence, no data-dependent loops): edge
+    // ee enters chain A iff ee <= hiA and chain B iff loB <= ee <= hiB, as fmaf(v, 1, acc)
+    // (= acc + v, one rounding) or fmaf(v, 0, acc) (= acc exactly: a chain never holds -0, and
+    // messages are finite GELU outputs).
+    const int rA = (32 * blk) / 50;                    // wave-uniform
+    const int lastA = 50 * (rA + 1) - 1 - 32 * blk;    // block-local index of rA's last edge
+    const int j0 = 32 * blk - 50 * rA;                 // slot of the block's edge 0 within rA
+    const int degA = a.deg[g0 + rA];
+    const int degB = rA + 1 < 32 ? a.deg[g0 + rA + 1] : 0;
+    const int hiA = min(min(lastA, 31), degA - 1 - j0);  // chain A sums edges [0, hiA]
+    const int loB = lastA + 1;                           // chain B sums edges [loB, hiB]
+    const int hiB = min(31, lastA + degB);
+    // wave-uniform edge masks of the two chains (bit ee set = edge ee enters the chain)
+    const uint32_t mA = (uint32_t)__builtin_amdgcn_readfirstlane(
+        hiA < 0 ? 0u : (hiA >= 31 ? 0xffffffffu : (1u << (hiA + 1)) - 1u));
+    const uint32_t mB = (uint32_t)__builtin_amdgcn_readfirstlane(
+        loB > hiB ? 0u : ((hiB >= 31 ? 0xffffffffu : (1u << (hiB + 1)) - 1u) & ~((1u << loB) - 1u)));
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int Mh = 0; Mh < 2; ++Mh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lc = 32 * Mh + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          scratch[lc * 36 + (lane & 31)] = m.m[2 * p + Mh][r];
+        }
+      __builtin_amdgcn_wave_barrier();
+      const float4* srow = reinterpret_cast<const float4*>(scratch + lane * 36);
+      float v[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 t = srow[q];
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      }
+      float accA = carry[p], accB = 0.0f;
+      seg_chains(v, mA, mB, accA, accB, std::make_integer_sequence<int, 32>{});
+      __builtin_amdgcn_wave_barrier();
+      if (lastA <= 31) {
+        aggl[rA * 128 + perm_pos(64 * p + lane)] = accA;
+        carry[p] = lastA < 31 ? accB : 0.0f;
+      } else {
+        carry[p] = accA;
+      }
+    }
+  }
+}
+
+// The node phase of one fused-layer task (lane&31 = receiver of g0 .. g0+31), the sums at aggl: the
+// body node_update had, forced inline into the kernels (calling node_update from k_mpnn made the
+// compiler spill 45 VGPRs in k_mpnn<1,2>).
+template <int LAYER>
+__device__ __forceinline__ void mpnn_node_tile(const MpnnArgs& a, int64_t g0, int lane, const float* aggl) {
+  const int64_t gl = g0 + (lane & 31);
+  Tile x;
+  {
+    Tile ag;
+    agg_from_gsum(ag, aggl + (lane & 31) * 128, a.deg[gl], a.msg);
+    if (LAYER == 0) {
+      int lr = a.node_local[gl];
+      tile_load_perm(x, a.h0tab + (int64_t)(lr < 0 ? 0 : lr) * 128);
+    } else {
+      tile_load_perm(x, a.h_in + gl * 128);
+    }
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x.m[M][r] = x.m[M][r] + ag.m[M][r] / 50.0f;
+  }
+  tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0
+  Tile out;
+  for (int ck = 0; ck < 4; ++ck) {
+    Tile hid;
+    tile_gemm_bf(hid, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, ActId{});
+    if (ck == 0)
+      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu{});
+    else
+      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu{});
+  }
+  tile_add(x, out);
+  tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
+  tile_store_perm(x, a.h_out + gl * 128);
+  if (a.P_out) {
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+      Tile pr;
+      if (p & 1) {  // receiver parts chain from the layer's first-layer bias
+        tile_gemm_bf(pr, x, a.proj_w + p * 64 * 64, a.proj_bf[p >> 1], ActId{});
+      } else {
+        tile_zero(pr);
+        tile_gemm(pr, x, a.proj_w + p * 64 * 64);
+      }
+      tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
+    }
+  }
+}
+
 // Fused layer (large batches): one wave per task runs its 50 edge blocks in order, carrying the
 // ordered segment sums in registers/LDS, then the node update. No per-edge message traffic.
 // HALF (batches of at most one round of tasks): two waves per task, wave 2t+h running edge
@@ -794,6 +912,73 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
         tile_gemm(pr, x, a.proj_w + p * 64 * 64);
       }
       tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
+    }
+  }
+}
+
+// Fused layer as a persistent work queue (batches of more than one round of tasks). The unit of
+// work is HALF a task — edge blocks 25h .. 25h+24, exactly receivers 16h .. 16h+15 (as in
+// k_mpnn<L, true>) — so the last units of a launch are half as long as whole tasks and the
+// layer's tail shrinks with them; every wave slot pulls units until the queues are empty. The
+// wave that completes the SECOND half of a task (told by the value its add on the task's counter
+// returns) runs the task's node update alone, as k_mpnn<L, false> does. Same operations in the
+// same order as the other fused forms: identical bits.
+// Queues: one per XCD (tasks split into 8 contiguous ranges, units 2t, 2t+1 = the halves of task
+// t), a wave pulls from its own XCD's queue (s_getreg XCC_ID; locality only) and, once that is
+// empty, from the next ones in turn; it leaves after finding all eight empty (every exit path is
+// bounded: one failed pull per queue). The halves of a task may run on different XCDs, so the
+// segment-sum hand-off is the agent-scope release / acquire pair (MI355X_MICROARCH.md,
+// inter-workgroup visibility): the producer's stores drained, release, then the counter add;
+// the consumer's acquire after its add returned. q_head / q_done are zeroed before each launch.
+// The kernel arguments are re-read through an opaque pointer to the kernarg segment at every unit
+// (scalar loads), so the compiler does not keep ~70 argument registers live across the queue
+// loop (carried, they spilled 43 VGPRs and 149 SGPRs).
+typedef const MpnnArgs __attribute__((address_space(4)))* MpnnArgsK;
+
+template <int LAYER>
+__global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_q(MpnnArgs a_in) {
+  (void)a_in;
+  const MpnnArgsK a_k = (MpnnArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+  __shared__ float lds_scratch[4][64 * 36];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int KL = w1_lds_ksteps<LAYER>();
+  __shared__ float4 w1_lds_buf[(KL > 0 ? KL : 1) * 64];
+  const float4* w1_lds = KL > 0 ? w1_lds_buf : nullptr;
+  if (KL > 0) {
+    for (int i = threadIdx.x; i < KL * 64; i += 256) w1_lds_buf[i] = a_k->msg.w1[i];
+    __syncthreads();
+  }
+  // HW_REG_XCC_ID (hwreg 20): bits 0-3 = this wave's XCD
+  int q = __builtin_amdgcn_readfirstlane((int)(__builtin_amdgcn_s_getreg(0xf814) & 7));
+  int empty = 0;
+  while (empty < 8) {
+    MpnnArgsK ap = a_k;
+    asm volatile("" : "+s"(ap));
+    const MpnnArgs& a = *(const MpnnArgs*)ap;
+    int j = 0;
+    if (lane == 0) j = __hip_atomic_fetch_add(a.q_head + 16 * q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    j = __builtin_amdgcn_readfirstlane(j);
+    const int64_t t0 = a.n_tasks * q / 8, t1 = a.n_tasks * (q + 1) / 8;
+    if (j >= 2 * (t1 - t0)) {
+      ++empty;
+      q = (q + 1) & 7;
+      continue;
+    }
+    const int64_t task = t0 + (j >> 1);
+    const int hh = j & 1;
+    mpnn_edge_blocks<LAYER>(a, task, lane, 25 * hh, 25 * hh + 25, w1_lds, lds_scratch, w);
+    // hand-off of this half's segment sums: stores drained, agent release, then the counter
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(a.q_done + task, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev == 1) {  // both halves done: this wave runs the node update
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      mpnn_node_tile<LAYER>(a, task * 32, lane, a.agg + task * 32 * 128);
     }
   }
 }
@@ -1707,6 +1892,14 @@ void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st) {
     else if (layer == 0) hipLaunchKernelGGL(k_mpnn_node<0>, grid, dim3(256), 0, st, a);
     else if (layer == 1) hipLaunchKernelGGL(k_mpnn_node<1>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_mpnn_node<2>, grid, dim3(256), 0, st, a);
+    return;
+  }
+  if (a.q_head) {  // persistent half-task queue: every wave slot, at most one unit per wave
+    const int64_t units = 2 * a.n_tasks;
+    const dim3 qgrid((unsigned)std::min<int64_t>((units + 3) / 4, a.q_grid));
+    if (layer == 0) hipLaunchKernelGGL(k_mpnn_q<0>, qgrid, dim3(256), 0, st, a);
+    else if (layer == 1) hipLaunchKernelGGL(k_mpnn_q<1>, qgrid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_mpnn_q<2>, qgrid, dim3(256), 0, st, a);
     return;
   }
   if (a.half_tasks) {  // two waves per task (n_tasks % 4 == 0: run() pads slots to 128)

@@ -500,6 +500,40 @@ void parse_texts(int32_t n, const char* const* texts, const size_t* lens, char c
 
 }  // namespace
 
+namespace {
+// positions as double (pst_pdb_batch_copy) or float (pst_pdb_batch_copy_f32: the parser's values are
+// float32 already, Bio's atom.coord, so the float copy is exact and half the bytes)
+template <typename T>
+int batch_copy(const pst_pdb_batch* b, T* positions, uint8_t* flags, uint8_t* aatype, int64_t* offsets,
+               int32_t* status) {
+  if (!b) return PST_E_INVALID;
+  const int32_t n = (int32_t)b->items.size();
+  std::vector<int64_t> off(n + 1, 0);
+  for (int32_t i = 0; i < n; ++i) off[i + 1] = off[i] + b->items[i].n;
+  if (offsets) memcpy(offsets, off.data(), sizeof(int64_t) * (n + 1));
+  for (int32_t i = 0; i < n; ++i)
+    if (status) status[i] = b->items[i].status;
+  // the copies (~925 B per residue) on a few threads once there are megabytes of them
+  const int threads = off[n] * (37 + 111 * (int64_t)sizeof(T)) > (4 << 20) ? 8 : 1;
+  run_pool(n, threads, [&](int i) { return (size_t)b->items[i].n; }, [&](int i) {
+    const Parsed& it = b->items[i];
+    const int64_t r = off[i];
+    if (positions && it.n) {
+      if (sizeof(T) == sizeof(double)) {
+        memcpy(positions + r * 111, it.pos.data(), sizeof(double) * 111 * it.n);
+      } else {
+        const double* src = it.pos.data();
+        T* dst = positions + r * 111;
+        for (int64_t k = 0; k < 111 * (int64_t)it.n; ++k) dst[k] = (T)src[k];
+      }
+    }
+    if (flags && it.n) memcpy(flags + r * 37, it.flags.data(), 37 * it.n);
+    if (aatype && it.n) memcpy(aatype + r, it.aatype.data(), it.n);
+  });
+  return PST_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int pst_pdb_parse_strings(const char* const* texts, const size_t* lens, int32_t n, char chain_id, int32_t n_threads,
@@ -549,23 +583,12 @@ int pst_pdb_batch_sizes(const pst_pdb_batch* b, int32_t* n, int64_t* n_residues)
 
 int pst_pdb_batch_copy(const pst_pdb_batch* b, double* positions, uint8_t* flags, uint8_t* aatype, int64_t* offsets,
                        int32_t* status) {
-  if (!b) return PST_E_INVALID;
-  const int32_t n = (int32_t)b->items.size();
-  std::vector<int64_t> off(n + 1, 0);
-  for (int32_t i = 0; i < n; ++i) off[i + 1] = off[i] + b->items[i].n;
-  if (offsets) memcpy(offsets, off.data(), sizeof(int64_t) * (n + 1));
-  for (int32_t i = 0; i < n; ++i)
-    if (status) status[i] = b->items[i].status;
-  // the copies (~925 B per residue) on a few threads once there are megabytes of them
-  const int threads = off[n] * 925 > (4 << 20) ? 8 : 1;
-  run_pool(n, threads, [&](int i) { return (size_t)b->items[i].n; }, [&](int i) {
-    const Parsed& it = b->items[i];
-    const int64_t r = off[i];
-    if (positions && it.n) memcpy(positions + r * 111, it.pos.data(), sizeof(double) * 111 * it.n);
-    if (flags && it.n) memcpy(flags + r * 37, it.flags.data(), 37 * it.n);
-    if (aatype && it.n) memcpy(aatype + r, it.aatype.data(), it.n);
-  });
-  return PST_OK;
+  return batch_copy(b, positions, flags, aatype, offsets, status);
+}
+
+int pst_pdb_batch_copy_f32(const pst_pdb_batch* b, float* positions, uint8_t* flags, uint8_t* aatype,
+                           int64_t* offsets, int32_t* status) {
+  return batch_copy(b, positions, flags, aatype, offsets, status);
 }
 
 const char* pst_pdb_batch_error(const pst_pdb_batch* b, int32_t i) {

@@ -40,7 +40,7 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free", "pst_write_files",
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
            "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_decode_ex", "pst_decoder_debug",
-           "pst_build_graph", "pst_clock_probe_start", "pst_clock_probe_stop")
+           "pst_build_graph", "pst_clock_probe_start", "pst_clock_probe_stop", "pst_pdb_batch_copy_f32")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -94,6 +94,7 @@ def lib():
         L.pst_pdb_parse_strings.argtypes = [P, P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_batch_sizes.argtypes = [P, P, P]
         L.pst_pdb_batch_copy.argtypes = [P, P, P, P, P, P]
+        L.pst_pdb_batch_copy_f32.argtypes = [P, P, P, P, P, P]
         L.pst_pdb_batch_error.restype = ctypes.c_char_p
         L.pst_pdb_batch_error.argtypes = [P, ctypes.c_int32]
         L.pst_pdb_batch_free.argtypes = [P]
@@ -157,35 +158,38 @@ class PdbBatch(NamedTuple):
                                       ((fl >> 1) & 1).astype(bool), 0.0, 1)
 
 
-def _collect_pdb(h) -> PdbBatch:
+def _collect_pdb(h, f32: bool = False) -> PdbBatch:
     L = lib()
     try:
         n = ctypes.c_int32()
         r = ctypes.c_int64()
         L.pst_pdb_batch_sizes(h, ctypes.byref(n), ctypes.byref(r))
         n, r = n.value, r.value
-        # every element is written by pst_pdb_batch_copy (absent atoms as 0.0)
-        pos = np.empty((r, 37, 3), np.float64)
+        # every element is written by pst_pdb_batch_copy(_f32) (absent atoms as 0.0)
+        pos = np.empty((r, 37, 3), np.float32 if f32 else np.float64)
         fl = np.empty((r, 37), np.uint8)
         aa = np.empty(r, np.uint8)
         off = np.zeros(n + 1, np.int64)
         st = np.zeros(n, np.int32)
-        L.pst_pdb_batch_copy(h, _ptr(pos), _ptr(fl), _ptr(aa), _ptr(off), _ptr(st))
+        copy = L.pst_pdb_batch_copy_f32 if f32 else L.pst_pdb_batch_copy
+        copy(h, _ptr(pos), _ptr(fl), _ptr(aa), _ptr(off), _ptr(st))
         errs = [L.pst_pdb_batch_error(h, i).decode() for i in range(n)]
     finally:
         L.pst_pdb_batch_free(h)
     return PdbBatch(pos, fl, aa, off, st, errs)
 
 
-def parse_pdb_files(paths: Sequence[str], chain_id: Optional[str] = None, n_threads: int = 8) -> PdbBatch:
-    """Parse PDB files on n_threads host threads with the native parser (pst_pdb_parse_files)."""
+def parse_pdb_files(paths: Sequence[str], chain_id: Optional[str] = None, n_threads: int = 8,
+                    float32: bool = False) -> PdbBatch:
+    """Parse PDB files on n_threads host threads with the native parser (pst_pdb_parse_files).
+    `float32`: positions as float32 (exact; pst_pdb_batch_copy_f32), the input pst_tokenize_f32 takes."""
     enc = [os.fsencode(p) for p in paths]
     arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
     h = ctypes.c_void_p()
     rc = lib().pst_pdb_parse_files(arr, len(enc), (chain_id or "\0").encode()[:1], n_threads, ctypes.byref(h))
     if rc != PST_OK:
         raise PstError(f"pst_pdb_parse_files failed: {rc}")
-    return _collect_pdb(h)
+    return _collect_pdb(h, float32)
 
 
 def parse_pdb_strings(texts: Sequence[str], chain_id: Optional[str] = None, n_threads: int = 8) -> PdbBatch:
@@ -384,11 +388,12 @@ class Tokenizer:
 
     def last_plan_detail(self) -> dict:
         """The last host-buffer tokenize call's plan: copy ranges, chunks, the chunks' protein cuts
-        and each chunk's layer schedule ("fused", "fused_half" = two waves per task, "split")."""
+        and each chunk's layer schedule ("fused", "fused_half" = two waves per task, "split",
+        "fused_queue" = the persistent half-task queue)."""
         out = np.zeros(20, np.int32)
         self._check(lib().pst_debug_fetch(self._h, 20, _ptr(out), out.nbytes))
         C = int(out[1])
-        names = {0: "fused", 1: "fused_half", 2: "split"}
+        names = {0: "fused", 1: "fused_half", 2: "split", 3: "fused_queue"}
         return {"ranges": int(out[0]), "chunks": C, "cuts": [int(x) for x in out[2:3 + C]],
                 "schedules": [names[int(x)] for x in out[11:11 + C]],
                 "downsampler": {0: "one_wave", 1: "coop", 2: "pair"}[int(out[19])]}

@@ -226,12 +226,13 @@ def test_invalid_inputs_rejected():
     assert np.array_equal(tk.tokenize([s])[0], O.tokenize(P.random_blob(6, 1234), LEVELS[4096], 1, s.atom37_positions, s.atom_flags())["tokens"])
 
 
-@pytest.mark.parametrize("split,half", [("0", "0"), ("0", "1"), ("1000000", "0")])
-def test_fused_and_split_layers_identical(split, half, monkeypatch):
+@pytest.mark.parametrize("split,half,queue", [("0", "0", "0"), ("0", "1", "0"), ("1000000", "0", "0"),
+                                              ("0", "0", "1")])
+def test_fused_and_split_layers_identical(split, half, queue, monkeypatch):
     """The MPNN schedules (fused: one wave per 32 receivers; fused with two waves per task, 16
-    receivers each; split: edge blocks spread over the GPU, messages through HBM) give the same
-    bits. Small batches default to split, so this forces each mode in a fresh context and
-    compares with the oracle-checked default."""
+    receivers each; split: edge blocks spread over the GPU, messages through HBM; fused as the
+    persistent half-task queue, k_mpnn_q) give the same bits. Small batches default to split, so
+    this forces each mode in a fresh context and compares with the oracle-checked default."""
     from pst_amd._native import Tokenizer, pack_samples
     samples = [synthetic.synthetic_protein(n, 300 + n) for n in (50, 99, 256, 512, 131)]
     pos, flags, off = pack_samples(samples)
@@ -241,9 +242,12 @@ def test_fused_and_split_layers_identical(split, half, monkeypatch):
     hl2 = [ref.debug_fetch(w, R) for w in (1, 2, 3)]
     monkeypatch.setenv("PST_SPLIT_TASKS", split)
     monkeypatch.setenv("PST_HALF_TASKS", half)
+    monkeypatch.setenv("PST_MPNN_QUEUE", queue)
     monkeypatch.setenv("PST_DEBUG", "1")
     tk = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
     tok, nt, nn = tk.tokenize_packed(pos, flags, off)
+    if queue == "1":
+        assert tk.last_plan_detail()["schedules"] == ["fused_queue"]
     hl = [tk.debug_fetch(w, R) for w in (1, 2, 3)]
     for a, b in zip(hl, hl2):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
@@ -342,3 +346,35 @@ def test_make_graph_from_pdb_reads_as_reference_graph(tmp_path):
                                    residue_loc_is_alphac=True, padding_num_residue=512)
     check_graph(v.graph, "casp_T1024_df1")
     assert np.array_equal(v.senders, v.graph.senders) and v.nb_residues == 391
+
+
+def test_mpnn_queue_identical_at_full_rounds(monkeypatch):
+    """k_mpnn_q at several rounds of tasks (3 072 tasks, ragged proteins so tasks straddle
+    proteins): the halves of a task are handed between waves that may sit on different XCDs
+    (agent release / acquire); node features after every layer, tokens and bounded latents must
+    equal the one-wave fused form bit for bit, on three calls of the same context (L1/L2 warm,
+    the counters re-zeroed per call)."""
+    from pst_amd._native import Tokenizer, pack_samples
+    rng = np.random.default_rng(5)
+    lens = [int(x) for x in rng.integers(60, 513, 340)]
+    samples = [synthetic.synthetic_protein(n, 4000 + i) for i, n in enumerate(lens)]
+    pos, flags, off = pack_samples(samples)
+    R = int(off[-1])
+    outs = []
+    monkeypatch.setenv("PST_DEBUG", "1")
+    monkeypatch.setenv("PST_H2D_CHUNKS", "1")
+    for queue in ("0", "1"):
+        monkeypatch.setenv("PST_MPNN_QUEUE", queue)
+        tk = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
+        for rep in range(3 if queue == "1" else 1):
+            tok, nt, nn = tk.tokenize_packed(pos.astype(np.float32), flags, off)
+            assert tk.last_plan_detail()["schedules"] == (["fused_queue"] if queue == "1" else ["fused"])
+            hl = [tk.debug_fetch(w, R) for w in (1, 2, 3)]
+            outs.append((tok[:R].copy(), [h.view(np.uint32).copy() for h in hl], tk.aux(R)["bounded"].view(np.uint32)))
+        tk.close()
+    base = outs[0]
+    for o in outs[1:]:
+        assert np.array_equal(o[0], base[0])
+        for a, b in zip(o[1], base[1]):
+            assert np.array_equal(a, b)
+        assert np.array_equal(o[2], base[2])

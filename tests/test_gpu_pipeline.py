@@ -168,18 +168,18 @@ def test_clock_probe_runs_beside_tokenize_and_stops():
     """pst_clock_probe_start/stop (bench.py's clock field): the probe wave samples while a
     tokenize call runs on the context's stream, stops when asked, and the clock it implies is a
     plausible gfx950 shader clock; a second start while running and a stop without a probe are
-    PST_E_INVALID. The tokens are the same with and without the probe."""
-    from pst_amd._native import PstError, Tokenizer
+    PST_E_INVALID (ValueError). The tokens are the same with and without the probe."""
+    from pst_amd._native import Tokenizer
     samples = synthetic.synthetic_batch(64, 256, seed=1000)
     pos, flags, off = pack_samples(samples)
     t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
     tok0, _, _ = t.tokenize_packed(pos, flags, off)
     t.clock_probe_start(max_samples=4096, sleep_units=4)
-    with pytest.raises(PstError):
+    with pytest.raises(ValueError, match="already running"):
         t.clock_probe_start(max_samples=4096, sleep_units=4)
     tok1, _, _ = t.tokenize_packed(pos, flags, off)
     s = t.clock_probe_stop()
-    with pytest.raises(PstError):
+    with pytest.raises(ValueError, match="no clock probe"):
         t.clock_probe_stop()
     t.close()
     assert np.array_equal(tok0, tok1)

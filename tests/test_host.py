@@ -396,3 +396,22 @@ def test_native_parser_multichunk_matches_restatement(case):
         assert nat.status[0] != 0 and nat.errors[0].startswith("malformed ATOM/HETATM record")
         return
     _both(txt)
+
+
+def test_parse_float32_copy_is_exact():
+    """pst_pdb_batch_copy_f32: the parser's coordinates are float32 values (Bio's atom.coord),
+    so the float32 copy-out equals the float64 one exactly; flags, aatype and offsets equal."""
+    import tarfile
+    import tempfile
+    from pst_amd._native import parse_pdb_files
+    arc = os.path.join(os.path.dirname(__file__), "golden", "casp14_pdbs.tar.gz")
+    with tempfile.TemporaryDirectory() as d:
+        with tarfile.open(arc) as tf:
+            tf.extractall(d, members=[m for m in tf.getmembers() if m.isfile() and m.name.endswith(".pdb")])
+        files = sorted(os.path.join(d, "casp14_pdbs", f) for f in os.listdir(os.path.join(d, "casp14_pdbs")))
+        a = parse_pdb_files(files, n_threads=4)
+        b = parse_pdb_files(files, n_threads=4, float32=True)
+    assert b.positions.dtype == np.float32
+    assert np.array_equal(b.positions.astype(np.float64), a.positions)
+    for k in ("flags", "aatype", "offsets", "status"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
