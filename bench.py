@@ -268,68 +268,22 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
                        "make_forward_bench.py; tests/golden/forward_ref_wide.npz, make_forward_wide.py)"}
 
 
-def clock_stats(samples, window_ms=1.0):
-    """Shader clock from the probe's (s_memtime, s_memrealtime @ 100 MHz) stamps: the mean over the
-    probed span (total cycles / total time) and the slowest `window_ms` window."""
-    if samples is None or len(samples) < 3:
+def clock_stats(per_step):
+    """Shader clock from libpst's clock counters (pst_clock_counters): per step, the stamping wave
+    of each fused MPNN launch contributes (s_memtime cycles, s_memrealtime 100 MHz ticks); the
+    step's clock = cycles / ticks x 0.1 GHz over its three layers (~90 % of the step's device
+    time). Mean (cycle-weighted over all steps), min and max over steps, per-layer means."""
+    if not per_step:
         return None
-    s = samples.astype(np.float64)
-    dc, dw = np.diff(s[:, 0]), np.diff(s[:, 1])
-    ok = dw > 0
-    dc, dw = dc[ok], dw[ok]
-    mean = float(dc.sum() / dw.sum() * 0.1)
-    t = np.cumsum(dw) / 1e5  # ms
-    win = np.floor(t / window_ms).astype(np.int64)
-    wc = np.bincount(win, weights=dc)
-    ww = np.bincount(win, weights=dw)
-    full = ww >= 0.5 * window_ms * 1e5
-    per = wc[full] / ww[full] * 0.1 if full.any() else np.array([mean])
-    return {"mean_ghz": round(mean, 4), "min_ghz": round(float(per.min()), 4),
-            "p10_ghz": round(float(np.percentile(per, 10)), 4), "p90_ghz": round(float(np.percentile(per, 90)), 4),
-            "span_ms": round(float(t[-1]), 1), "samples": int(len(samples)), "window_ms": window_ms}
-
-
-def casp14_end_to_end(tk):
-    """SURVEY config 2 as the CLI runs it: parse the 31 CASP14 PDB files (native parser), tokenize
-    from host buffers, write <stem>_tokens.npy. Reported beside `value`."""
-    import tarfile
-    import tempfile
-    from pst_amd._native import parse_pdb_files
-    from pst_amd.runner import save_npy_files
-    arc = os.path.join(ROOT, "tests", "golden", "casp14_pdbs.tar.gz")
-    if not os.path.exists(arc):
-        return None, None
-    threads = min(16, host_cores())
-    # inputs and token files on tmpfs where there is one: the figure is the software path (parse,
-    # H2D + tokenize, .npy encode + write syscalls), not the speed of the box's disk
-    shm = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
-    with tempfile.TemporaryDirectory(dir=shm) as d:
-        with tarfile.open(arc) as tf:
-            tf.extractall(d, members=[m for m in tf.getmembers() if m.isfile() and m.name.endswith(".pdb")])
-        files = sorted(os.path.join(d, "casp14_pdbs", f) for f in os.listdir(os.path.join(d, "casp14_pdbs")))
-        runs = []
-        for rep in range(6):  # first pass warms the page cache and the context's workspace
-            out = os.path.join(d, f"out{rep}")
-            os.makedirs(out)
-            t0 = time.perf_counter()
-            B = parse_pdb_files(files, n_threads=threads, float32=True)  # exact: Bio's float32 coords
-            t1 = time.perf_counter()
-            tok, nt, _ = tk.tokenize_packed(B.positions, B.flags, B.offsets)
-            t2 = time.perf_counter()
-            save_npy_files([os.path.join(out, os.path.basename(f)[:-4] + "_tokens") for f in files],
-                           [tok[int(B.offsets[i]):int(B.offsets[i]) + nt[i]].reshape(1, -1) for i in range(len(files))])
-            t3 = time.perf_counter()
-            if rep:
-                runs.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2))
-        R = int(B.offsets[-1])
-        casp = (B.positions.astype(np.float64), np.array(B.flags), np.array(B.offsets), (tok.copy(), np.array(nt)))
-        tot, parse, tok, write = runs[int(np.argsort([r[0] for r in runs])[len(runs) // 2])]  # median run
-        res = {"workload": "CASP14 31 structures (SURVEY config 2), codebook 4096, df 1", "residues": R,
-               "parse_ms": round(parse * 1e3, 2), "tokenize_ms": round(tok * 1e3, 2),
-               "write_ms": round(write * 1e3, 2), "residues_per_s": round(R / tot, 1),
-               "parse_threads": threads, "runs": f"median of {len(runs)} after one warm-up",
-               "files_on": shm or tempfile.gettempdir()}
-    return res, casp
+    c = np.array(per_step, np.float64)  # [steps, 3, 2]
+    if c[..., 1].sum() <= 0:
+        return None
+    step = c[:, :, 0].sum(1) / np.maximum(c[:, :, 1].sum(1), 1) * 0.1
+    layer = c[:, :, 0].sum(0) / np.maximum(c[:, :, 1].sum(0), 1) * 0.1
+    return {"mean_ghz": round(float(c[..., 0].sum() / c[..., 1].sum() * 0.1), 4),
+            "min_ghz": round(float(step.min()), 4), "max_ghz": round(float(step.max()), 4),
+            "per_layer_ghz": [round(float(x), 4) for x in layer], "steps": len(per_step),
+            "stamped_ms": round(float(c[..., 1].sum() / 1e5), 1)}
 
 
 def _ref_as_computed_rate(model, pf, df, threads, cores, what):
@@ -480,20 +434,21 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    # shader clock over the timed steps: one probe wave on the context's own side stream
-    # (pst_clock_probe_start/stop), started before and stopped after the bracketed region
-    tk.clock_probe_start(max_samples=1 << 18, sleep_units=4)
-    times = []
+    # shader clock of every timed step from libpst's clock counters (pst_clock_counters: stamps
+    # of the fused MPNN launches), read between steps, outside each step's own timing
+    tk.clock_counters(reset=True)
+    times, clk = [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         t0 = time.perf_counter()
         tok, nt, nn = tk.tokenize_packed(ppos, pflags, off)  # host → host, synchronous
         times.append(time.perf_counter() - t0)
+        clk.append(tk.clock_counters(reset=True))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    clock = clock_stats(tk.clock_probe_stop())
+    clock = clock_stats(clk)
     plan = tk.last_plan_detail()  # chunks and layer schedule of the timed step (rank 0's share)
     log(f"rank {rank}: {args.steps} timed steps in {elapsed:.2f} s")
     stats = torch.tensor(times + [elapsed], dtype=torch.float64, device=red_dev)
@@ -552,12 +507,14 @@ def main():
         dts.append(time.perf_counter() - t0)
     tk.set_timing(True)
     stage = None
-    tk.clock_probe_start(max_samples=1 << 16, sleep_units=4)
+    sclk = []
+    tk.clock_counters(reset=True)
     for _ in range(3):
         dstep()
         st = tk.stage_ms()
         stage = st if stage is None else {k: stage[k] + st[k] for k in st}
-    stage_clock = clock_stats(tk.clock_probe_stop())
+        sclk.append(tk.clock_counters(reset=True))
+    stage_clock = clock_stats(sclk)
     stage = {k: v / 3 for k, v in stage.items()}
     tk.set_timing(False)
 
@@ -588,10 +545,11 @@ def main():
                 "FLOPs instead, which the kernel's algebraic rewrites (DESIGN.md 5) execute in 0.52x the work",
         "launch_ms": round(dom_ms, 3),
         "effective_alg_tflops": round(MPNN1_ALG_FLOP_PER_RES * R / (dom_ms * 1e-3) / 1e12, 2),
-        # the peak is quoted at the 2.4 GHz spec clock; at the clock the chip actually held over
-        # the stage-timing steps (probe, mean) the reachable peak is peak x clock / 2.4
+        # the peak is quoted at the 2.4 GHz spec clock; at the clock the chip actually held under
+        # k_mpnn<1> in the stage-timing steps (its launches' clock stamps) the reachable peak is
+        # peak x clock / 2.4
         "stage_clock": stage_clock,
-        "frac_at_measured_clock": (round(executed / (PEAK_FP32_TFLOPS * stage_clock["mean_ghz"] / SPEC_GHZ), 4)
+        "frac_at_measured_clock": (round(executed / (PEAK_FP32_TFLOPS * stage_clock["per_layer_ghz"][1] / SPEC_GHZ), 4)
                                    if stage_clock else None),
         "kernels": kern,
         "stage_ms": {k: round(v, 3) for k, v in stage.items()},
@@ -642,9 +600,10 @@ def main():
                                 "note": "rank 0's shard with inputs already in HBM (pst_tokenize_device), median of 5"},
             "clock": clock,
             "ms_per_step_at_2p4ghz": (round(med * 1e3 * clock["mean_ghz"] / SPEC_GHZ, 3) if clock else None),
-            "clock_note": ("shader clock over the timed steps (rank 0), one probe wave stamping s_memtime / "
-                           "s_memrealtime on a side stream (pst_clock_probe_start/stop); ms_per_step_at_2p4ghz "
-                           "scales the step as if all of it ran at the clock (the H2D part does not)"),
+            "clock_note": ("shader clock of the timed steps (rank 0): s_memtime / s_memrealtime stamps of the "
+                           "fused MPNN launches (pst_clock_counters), per step over its three layers; "
+                           "ms_per_step_at_2p4ghz scales the median step by mean_ghz / 2.4 as if all of it "
+                           "were clock-bound (the H2D part is not)"),
             "roofline": roofline,
             "exact_match_reference": ref_match,
             "exact_match": exact,

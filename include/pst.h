@@ -257,15 +257,13 @@ int pst_write_files(int32_t n, const char* const* paths, const void* const* data
 int pst_set_timing(pst_ctx* ctx, int32_t enable);
 int pst_get_timing(pst_ctx* ctx, float* ms);
 
-/* Clock probe (measurement only; bench.py reports the shader clock its timed steps ran at). start
- * launches ONE wave on a stream of the context's own that stamps (s_memtime, s_memrealtime) every
- * ~sleep_units x 8 K shader cycles, concurrently with whatever the context runs next; stop raises
- * a host-mapped flag the wave polls, waits for it and copies the n_samples (<= max_samples) stamp
- * pairs to samples[2*i], samples[2*i+1]. The shader clock between two samples is
- * d(memtime) / d(memrealtime) x 100 MHz. PST_E_INVALID if a probe is already running (start) or
- * none is (stop). */
-int pst_clock_probe_start(pst_ctx* ctx, int32_t max_samples, int32_t sleep_units);
-int pst_clock_probe_stop(pst_ctx* ctx, uint64_t* samples, int32_t max_samples, int32_t* n_samples);
+/* Clock counters (measurement; bench.py reports the shader clock its timed steps ran at): the
+ * first wave of workgroup 0 of every fused MPNN launch (the persistent queue form lives as long as
+ * its launch) adds its s_memtime (shader clock) and s_memrealtime (100 MHz) deltas, per layer.
+ * out[2l], out[2l+1] = the sums for layer l = 0..2 since the last reset (waits for the context's
+ * stream); clock of layer l = out[2l] / out[2l+1] x 100 MHz. reset != 0 zeroes them after the read.
+ * Split-schedule layers (small batches) add nothing. */
+int pst_clock_counters(pst_ctx* ctx, uint64_t* out, int32_t reset);
 
 /* Stream the context launches on (hipStream_t), for event timing by callers. */
 void* pst_stream(pst_ctx* ctx);

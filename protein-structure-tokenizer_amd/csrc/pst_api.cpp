@@ -278,13 +278,9 @@ struct pst_ctx {
   bool timing = false;
   hipEvent_t ev[PST_N_STAGES + 1] = {};
   int64_t dbg_cap = 0;
-  // clock probe (measurement only, pst_clock_probe_start/stop): one wave on probe_stream
-  hipStream_t probe_stream = nullptr;
-  unsigned long long* d_probe = nullptr;  // [max][2] (s_memtime, s_memrealtime)
-  int* d_probe_count = nullptr;
-  int* h_probe_stop = nullptr;  // pinned, mapped: the host raises it, the probe wave polls it
-  int32_t probe_cap = 0;
-  bool probe_running = false;
+  // clock stamps of the fused MPNN launches (pst_clock_counters): per layer [shader cycles,
+  // 100 MHz ticks] summed over calls, added by the stamping wave of each launch
+  unsigned long long* d_clk = nullptr;
 };
 
 namespace {
@@ -429,6 +425,8 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   HIPCHK(hipMalloc(&ctx->d_U, 1023 * 128 * sizeof(float)));
   HIPCHK(hipMalloc(&ctx->d_RPE, (size_t)ctx->max_out * 128 * sizeof(float)));
   HIPCHK(hipMemcpy(ctx->d_RPE, rpe.data(), rpe.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&ctx->d_clk, 6 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(ctx->d_clk, 0, 6 * sizeof(unsigned long long)));
   float* a = ctx->d_arena;
   auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(a + o); };
   // h0 = nodePE·W + b; PM0 = [h0·W0[0:128] | b0 + h0·W0[128:256]] (message MLP of layer 0);
@@ -662,6 +660,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.msg_rows = msg_rows;
     m.blocks_per_wave = bpw;
     m.half_tasks = half ? 1 : 0;
+    m.clk = ctx->d_clk + 2 * l;
     if (queue) {
       m.q_head = w.qctr + l * (128 + n_tasks);
       m.q_done = m.q_head + 128;
@@ -797,47 +796,15 @@ int pst_get_timing(pst_ctx* ctx, float* ms) {
   return PST_OK;
 }
 
-int pst_clock_probe_start(pst_ctx* ctx, int32_t max_samples, int32_t sleep_units) {
+int pst_clock_counters(pst_ctx* ctx, uint64_t* out, int32_t reset) {
   if (!ctx) return PST_E_INVALID;
-  if (max_samples < 2 || sleep_units < 1 || ctx->probe_running) {
-    ctx->err = ctx->probe_running ? "clock probe already running" : "clock probe: max_samples >= 2, sleep_units >= 1";
-    return PST_E_INVALID;
-  }
   HIPCHK(hipSetDevice(ctx->device));
-  if (!ctx->probe_stream) {
-    HIPCHK(hipStreamCreateWithFlags(&ctx->probe_stream, hipStreamNonBlocking));
-    HIPCHK(hipHostMalloc((void**)&ctx->h_probe_stop, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
-    HIPCHK(hipMalloc((void**)&ctx->d_probe_count, sizeof(int)));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (out) HIPCHK(hipMemcpy(out, ctx->d_clk, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (reset) {
+    HIPCHK(hipMemsetAsync(ctx->d_clk, 0, 6 * sizeof(uint64_t), ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
   }
-  if (max_samples > ctx->probe_cap) {
-    if (ctx->d_probe) HIPCHK(hipFree(ctx->d_probe));
-    HIPCHK(hipMalloc((void**)&ctx->d_probe, sizeof(unsigned long long) * 2 * (size_t)max_samples));
-    ctx->probe_cap = max_samples;
-  }
-  __atomic_store_n(ctx->h_probe_stop, 0, __ATOMIC_SEQ_CST);
-  int* d_stop = nullptr;
-  HIPCHK(hipHostGetDevicePointer((void**)&d_stop, ctx->h_probe_stop, 0));
-  pst::launch_clock_probe(ctx->d_probe, ctx->d_probe_count, max_samples, sleep_units, d_stop, ctx->probe_stream);
-  HIPCHK(hipGetLastError());
-  ctx->probe_running = true;
-  return PST_OK;
-}
-
-int pst_clock_probe_stop(pst_ctx* ctx, uint64_t* samples, int32_t max_samples, int32_t* n_samples) {
-  if (!ctx) return PST_E_INVALID;
-  if (!ctx->probe_running || !samples || !n_samples) {
-    ctx->err = ctx->probe_running ? "null argument" : "no clock probe running";
-    return PST_E_INVALID;
-  }
-  HIPCHK(hipSetDevice(ctx->device));
-  __atomic_store_n(ctx->h_probe_stop, 1, __ATOMIC_SEQ_CST);
-  HIPCHK(hipStreamSynchronize(ctx->probe_stream));
-  ctx->probe_running = false;
-  int n = 0;
-  HIPCHK(hipMemcpy(&n, ctx->d_probe_count, sizeof(int), hipMemcpyDeviceToHost));
-  n = std::min(n, std::min<int32_t>(max_samples, ctx->probe_cap));
-  if (n > 0) HIPCHK(hipMemcpy(samples, ctx->d_probe, sizeof(unsigned long long) * 2 * (size_t)n, hipMemcpyDeviceToHost));
-  *n_samples = n;
   return PST_OK;
 }
 
@@ -939,14 +906,7 @@ int pst_destroy(pst_ctx* ctx) {
   for (hipEvent_t e : ctx->range_ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->idle_ev) (void)hipEventDestroy(ctx->idle_ev);
-  if (ctx->probe_stream) {
-    if (ctx->h_probe_stop) __atomic_store_n(ctx->h_probe_stop, 1, __ATOMIC_SEQ_CST);
-    (void)hipStreamSynchronize(ctx->probe_stream);
-    (void)hipStreamDestroy(ctx->probe_stream);
-  }
-  if (ctx->d_probe) (void)hipFree(ctx->d_probe);
-  if (ctx->d_probe_count) (void)hipFree(ctx->d_probe_count);
-  if (ctx->h_probe_stop) (void)hipHostFree(ctx->h_probe_stop);
+  if (ctx->d_clk) (void)hipFree(ctx->d_clk);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return PST_OK;

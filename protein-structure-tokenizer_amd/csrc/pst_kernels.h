@@ -91,6 +91,9 @@ struct MpnnArgs {
   int32_t* q_head;
   int32_t* q_done;
   int64_t q_grid;
+  // clock stamps (measurement): the first wave of workgroup 0 adds its s_memtime (shader clock)
+  // and s_memrealtime (100 MHz) deltas to clk[0], clk[1] (pst_clock_counters); null = off
+  unsigned long long* clk;
   // outputs
   float* e_out;  // blocked (null for the last layer)
   float* h_out;
@@ -169,11 +172,5 @@ void launch_fsq_aux(const FsqAuxArgs& a, int n_prot, hipStream_t st);
 // Y = (init or 0) + X·W (+ b): init / b perm-ordered 128-vectors (either may be null)
 void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, const float* init, float* Y,
                        int ldy, hipStream_t st);
-
-// Measurement only: one wave stamps (s_memtime, s_memrealtime) into out[2i], out[2i+1] every
-// ~sleep_units x 8 K cycles until *stop (host-mapped) is set or max_samples are taken; *count =
-// samples written. The clock between samples is d(memtime) / d(memrealtime) x 100 MHz.
-void launch_clock_probe(unsigned long long* out, int* count, int max_samples, int sleep_units, const int* stop,
-                        hipStream_t st);
 
 }  // namespace pst

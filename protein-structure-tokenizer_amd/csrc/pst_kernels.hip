@@ -765,6 +765,32 @@ __device__ __forceinline__ void mpnn_node_tile(const MpnnArgs& a, int64_t g0, in
   }
 }
 
+// Clock stamps of a fused MPNN launch (measurement, MpnnArgs::clk): the first wave of workgroup 0
+// reads the shader clock counter (s_memtime) and the 100 MHz real-time counter at its start and
+// end and adds both deltas to clk[0..1] (one lane, vector atomics). The clock over the wave's
+// lifetime = d(memtime) / d(memrealtime) x 100 MHz; for the persistent k_mpnn_q that wave lives
+// as long as the launch.
+struct ClockStamp {
+  uint64_t t0 = 0, r0 = 0;
+  bool on = false;
+  __device__ __forceinline__ void start(unsigned long long* clk) {
+    on = clk && blockIdx.x == 0 && threadIdx.x < 64;
+    if (on) {
+      t0 = __builtin_amdgcn_s_memtime();
+      r0 = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  __device__ __forceinline__ void stop(unsigned long long* clk) {
+    if (on) {
+      const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+      if (threadIdx.x == 0) {
+        atomicAdd(clk, (unsigned long long)(t1 - t0));
+        atomicAdd(clk + 1, (unsigned long long)(r1 - r0));
+      }
+    }
+  }
+};
+
 // Fused layer (large batches): one wave per task runs its 50 edge blocks in order, carrying the
 // ordered segment sums in registers/LDS, then the node update. No per-edge message traffic.
 // HALF (batches of at most one round of tasks): two waves per task, wave 2t+h running edge
@@ -775,6 +801,8 @@ __device__ __forceinline__ void mpnn_node_tile(const MpnnArgs& a, int64_t g0, in
 template <int LAYER, bool HALF>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   __shared__ float lds_scratch[4][64 * 36];
+  ClockStamp cs;
+  cs.start(a.clk);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (no waterfalls)
   const int64_t task = HALF ? (int64_t)blockIdx.x * 2 + (w >> 1) : (int64_t)blockIdx.x * 4 + w;
@@ -862,6 +890,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     // the node update on both waves of the pair, two output blocks each, tiles exchanged
     // through this pair's half of lds_scratch (free after the edge phase)
     node_update_pair<LAYER>(a, g0, hh, lds_scratch[w & 2]);
+    cs.stop(a.clk);
     return;
   } else {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -914,6 +943,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
       tile_store_perm(pr, a.P_out + gl * 512 + p * 128);
     }
   }
+  cs.stop(a.clk);
 }
 
 // Fused layer as a persistent work queue (batches of more than one round of tasks). The unit of
@@ -937,8 +967,9 @@ typedef const MpnnArgs __attribute__((address_space(4)))* MpnnArgsK;
 
 template <int LAYER>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_q(MpnnArgs a_in) {
-  (void)a_in;
   const MpnnArgsK a_k = (MpnnArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+  ClockStamp cs;
+  cs.start(a_in.clk);
   __shared__ float lds_scratch[4][64 * 36];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -981,6 +1012,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_q(MpnnArgs a_in) 
       mpnn_node_tile<LAYER>(a, task * 32, lane, a.agg + task * 32 * 128);
     }
   }
+  cs.stop(a_k->clk);
 }
 
 // Split layer (small batches, where one wave per 32 receivers cannot fill the GPU): the edge
@@ -1926,33 +1958,6 @@ void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float
                        int ldy, hipStream_t st) {
   int tiles = (n_rows + 31) / 32;
   hipLaunchKernelGGL(k_table_gemm, dim3((tiles + 3) / 4), dim3(256), 0, st, X, n_rows, Wf, b, init, Y, ldy);
-}
-
-// ---------------------------------------------------------------------------- clock probe
-// (measurement only, pst_clock_probe_start/stop; bench.py reports the shader clock the timed
-// steps ran at). Every exit path is bounded: at most max_samples iterations.
-__global__ __launch_bounds__(64) void k_clock_probe(unsigned long long* out, int* count, int max_samples,
-                                                    int sleep_units, const int* stop) {
-  int i = 0;
-  for (; i < max_samples; ++i) {
-    const unsigned long long c = __builtin_amdgcn_s_memtime();
-    const unsigned long long w = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0) {
-      out[2 * i] = c;
-      out[2 * i + 1] = w;
-    }
-    if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-      ++i;
-      break;
-    }
-    for (int k = 0; k < sleep_units; ++k) __builtin_amdgcn_s_sleep(127);
-  }
-  if (threadIdx.x == 0) *count = i;
-}
-
-void launch_clock_probe(unsigned long long* out, int* count, int max_samples, int sleep_units, const int* stop,
-                        hipStream_t st) {
-  hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, st, out, count, max_samples, sleep_units, stop);
 }
 
 }  // namespace pst

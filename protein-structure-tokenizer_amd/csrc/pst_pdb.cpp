@@ -514,7 +514,9 @@ int batch_copy(const pst_pdb_batch* b, T* positions, uint8_t* flags, uint8_t* aa
   for (int32_t i = 0; i < n; ++i)
     if (status) status[i] = b->items[i].status;
   // the copies (~925 B per residue) on a few threads once there are megabytes of them
-  const int threads = off[n] * (37 + 111 * (int64_t)sizeof(T)) > (4 << 20) ? 8 : 1;
+  // (the float32 form converts element by element: threads from 1 MB on)
+  const int64_t bytes = off[n] * (37 + 111 * (int64_t)sizeof(T));
+  const int threads = bytes > (sizeof(T) == sizeof(double) ? (4 << 20) : (1 << 20)) ? 8 : 1;
   run_pool(n, threads, [&](int i) { return (size_t)b->items[i].n; }, [&](int i) {
     const Parsed& it = b->items[i];
     const int64_t r = off[i];

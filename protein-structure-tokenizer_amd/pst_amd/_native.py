@@ -40,7 +40,7 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free", "pst_write_files",
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
            "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_decode_ex", "pst_decoder_debug",
-           "pst_build_graph", "pst_clock_probe_start", "pst_clock_probe_stop", "pst_pdb_batch_copy_f32")
+           "pst_build_graph", "pst_clock_counters", "pst_pdb_batch_copy_f32")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -88,8 +88,7 @@ def lib():
         L.pst_set_timing.argtypes = [P, ctypes.c_int32]
         L.pst_get_timing.argtypes = [P, P]
         L.pst_device_count.argtypes = [P]
-        L.pst_clock_probe_start.argtypes = [P, ctypes.c_int32, ctypes.c_int32]
-        L.pst_clock_probe_stop.argtypes = [P, P, ctypes.c_int32, P]
+        L.pst_clock_counters.argtypes = [P, P, ctypes.c_int32]
         L.pst_pdb_parse_files.argtypes = [P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_parse_strings.argtypes = [P, P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_batch_sizes.argtypes = [P, P, P]
@@ -314,18 +313,12 @@ class Tokenizer:
     def sync(self):
         self._check(lib().pst_sync(self._h))
 
-    def clock_probe_start(self, max_samples: int = 65536, sleep_units: int = 4):
-        """Start the shader-clock probe (pst_clock_probe_start): one wave on the context's probe
-        stream, one sample every ~sleep_units x 8 K cycles, until clock_probe_stop."""
-        self._probe_max = int(max_samples)
-        self._check(lib().pst_clock_probe_start(self._h, self._probe_max, int(sleep_units)))
-
-    def clock_probe_stop(self):
-        """Stop the probe -> (memtime, memrealtime) samples, uint64 [n, 2]."""
-        buf = np.zeros((self._probe_max, 2), np.uint64)
-        n = ctypes.c_int32(0)
-        self._check(lib().pst_clock_probe_stop(self._h, _ptr(buf), self._probe_max, ctypes.byref(n)))
-        return buf[:n.value]
+    def clock_counters(self, reset: bool = False) -> np.ndarray:
+        """(shader cycles, 100 MHz ticks) per fused MPNN layer summed since the last reset, uint64
+        [3, 2] (pst_clock_counters); clock of layer l = c[l, 0] / c[l, 1] x 0.1 GHz."""
+        out = np.zeros((3, 2), np.uint64)
+        self._check(lib().pst_clock_counters(self._h, _ptr(out), 1 if reset else 0))
+        return out
 
     def build_graph_packed(self, pos, flags, offsets):
         """Residue graphs of a packed batch (pst_build_graph): senders [R,50] int32 (node index

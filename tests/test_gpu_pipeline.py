@@ -164,27 +164,25 @@ def test_two_proteins_small_first():
         assert np.array_equal(o[0], outs[0][0])
 
 
-def test_clock_probe_runs_beside_tokenize_and_stops():
-    """pst_clock_probe_start/stop (bench.py's clock field): the probe wave samples while a
-    tokenize call runs on the context's stream, stops when asked, and the clock it implies is a
-    plausible gfx950 shader clock; a second start while running and a stop without a probe are
-    PST_E_INVALID (ValueError). The tokens are the same with and without the probe."""
+def test_clock_counters_accumulate_and_reset():
+    """pst_clock_counters (bench.py's clock fields): each fused MPNN launch's stamping wave adds
+    (shader cycles, 100 MHz ticks); two calls add about twice one call's ticks, reset zeroes them,
+    the implied clock is a plausible gfx950 shader clock, and the tokens are unaffected."""
     from pst_amd._native import Tokenizer
-    samples = synthetic.synthetic_batch(64, 256, seed=1000)
+    samples = synthetic.synthetic_batch(512, 256, seed=1000)  # fused layers (queue form)
     pos, flags, off = pack_samples(samples)
     t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
     tok0, _, _ = t.tokenize_packed(pos, flags, off)
-    t.clock_probe_start(max_samples=4096, sleep_units=4)
-    with pytest.raises(ValueError, match="already running"):
-        t.clock_probe_start(max_samples=4096, sleep_units=4)
+    t.clock_counters(reset=True)
+    assert not t.clock_counters().any()
     tok1, _, _ = t.tokenize_packed(pos, flags, off)
-    s = t.clock_probe_stop()
-    with pytest.raises(ValueError, match="no clock probe"):
-        t.clock_probe_stop()
+    c1 = t.clock_counters().astype(np.float64)
+    t.tokenize_packed(pos, flags, off)
+    c2 = t.clock_counters(reset=True).astype(np.float64)
+    assert not t.clock_counters().any()
     t.close()
     assert np.array_equal(tok0, tok1)
-    assert 3 <= len(s) <= 4096
-    dc = np.diff(s[:, 0].astype(np.float64))
-    dw = np.diff(s[:, 1].astype(np.float64))
-    ghz = dc.sum() / dw.sum() * 0.1
-    assert 0.3 < ghz < 3.0, ghz
+    assert (c1 > 0).all(), c1
+    ghz = c1[:, 0] / c1[:, 1] * 0.1
+    assert ((ghz > 0.3) & (ghz < 3.0)).all(), ghz
+    assert (np.abs(c2[:, 1] / c1[:, 1] - 2.0) < 0.5).all(), (c1, c2)
