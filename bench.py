@@ -275,7 +275,7 @@ def clock_stats(per_step):
     time). Mean (cycle-weighted over all steps), min and max over steps, per-layer means."""
     if not per_step:
         return None
-    c = np.array(per_step, np.float64)  # [steps, 3, 2]
+    c = np.array(per_step, np.float64)[:, :, :2]  # [steps, 3, (cycles, ticks)]
     if c[..., 1].sum() <= 0:
         return None
     step = c[:, :, 0].sum(1) / np.maximum(c[:, :, 1].sum(1), 1) * 0.1

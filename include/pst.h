@@ -257,12 +257,13 @@ int pst_write_files(int32_t n, const char* const* paths, const void* const* data
 int pst_set_timing(pst_ctx* ctx, int32_t enable);
 int pst_get_timing(pst_ctx* ctx, float* ms);
 
-/* Clock counters (measurement; bench.py reports the shader clock its timed steps ran at): the
- * first wave of workgroup 0 of every fused MPNN launch (the persistent queue form lives as long as
- * its launch) adds its s_memtime (shader clock) and s_memrealtime (100 MHz) deltas, per layer.
- * out[2l], out[2l+1] = the sums for layer l = 0..2 since the last reset (waits for the context's
- * stream); clock of layer l = out[2l] / out[2l+1] x 100 MHz. reset != 0 zeroes them after the read.
- * Split-schedule layers (small batches) add nothing. */
+/* Clock and occupancy counters of the fused MPNN launches (measurement; bench.py reports them).
+ * out[8l + i] for layer l = 0..2, over the calls since the last reset (waits for the context's
+ * stream): i = 0, 1: s_memtime (shader clock) and s_memrealtime (100 MHz) deltas of the first wave
+ * of workgroup 0 (clock = out[0] / out[1] x 100 MHz; the persistent queue form's waves live as
+ * long as the launch); 2: Σ wave lifetimes (100 MHz ticks); 3 / 4: earliest wave start / latest
+ * wave end; 5: waves (occupancy = out[2] / (wave slots x (out[4] - out[3]))); 6, 7: 0. reset != 0
+ * restarts them after the read. Split-schedule layers (small batches) add nothing. */
 int pst_clock_counters(pst_ctx* ctx, uint64_t* out, int32_t reset);
 
 /* Stream the context launches on (hipStream_t), for event timing by callers. */

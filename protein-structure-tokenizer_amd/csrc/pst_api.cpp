@@ -278,12 +278,14 @@ struct pst_ctx {
   bool timing = false;
   hipEvent_t ev[PST_N_STAGES + 1] = {};
   int64_t dbg_cap = 0;
-  // clock stamps of the fused MPNN launches (pst_clock_counters): per layer [shader cycles,
-  // 100 MHz ticks] summed over calls, added by the stamping wave of each launch
+  // clock stamps of the fused MPNN launches (pst_clock_counters): per layer 8 u64 — [shader cycles,
+  // 100 MHz ticks] of the stamping wave, Σ wave lifetimes, min wave start, max wave end, waves —
+  // summed over calls (min / max over calls)
   unsigned long long* d_clk = nullptr;
 };
 
 namespace {
+int reset_clock_counters(pst_ctx* ctx);  // below (pst_clock_counters)
 
 inline void mark(pst_ctx* ctx, int i) {
   if (ctx->timing) (void)hipEventRecord(ctx->ev[i], ctx->stream);
@@ -425,8 +427,8 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   HIPCHK(hipMalloc(&ctx->d_U, 1023 * 128 * sizeof(float)));
   HIPCHK(hipMalloc(&ctx->d_RPE, (size_t)ctx->max_out * 128 * sizeof(float)));
   HIPCHK(hipMemcpy(ctx->d_RPE, rpe.data(), rpe.size() * sizeof(float), hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&ctx->d_clk, 6 * sizeof(unsigned long long)));
-  HIPCHK(hipMemset(ctx->d_clk, 0, 6 * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&ctx->d_clk, 24 * sizeof(unsigned long long)));
+  if (int rc = reset_clock_counters(ctx)) return rc;
   float* a = ctx->d_arena;
   auto F4 = [&](size_t o) { return reinterpret_cast<const float4*>(a + o); };
   // h0 = nodePE·W + b; PM0 = [h0·W0[0:128] | b0 + h0·W0[128:256]] (message MLP of layer 0);
@@ -515,6 +517,15 @@ int ensure_workspace(pst_ctx* ctx, int64_t R, int B) {
   }
   ctx->cap_R = Rpad;
   ctx->cap_B = B;
+  return PST_OK;
+}
+
+// clock / occupancy counters (pst_clock_counters) to their start values: sums 0, min start ~0
+int reset_clock_counters(pst_ctx* ctx) {
+  uint64_t init[24] = {};
+  for (int l = 0; l < 3; ++l) init[8 * l + 3] = ~0ull;
+  HIPCHK(hipMemcpyAsync(ctx->d_clk, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   return PST_OK;
 }
 
@@ -660,7 +671,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.msg_rows = msg_rows;
     m.blocks_per_wave = bpw;
     m.half_tasks = half ? 1 : 0;
-    m.clk = ctx->d_clk + 2 * l;
+    m.clk = ctx->d_clk + 8 * l;
     if (queue) {
       m.q_head = w.qctr + l * (128 + n_tasks);
       m.q_done = m.q_head + 128;
@@ -800,12 +811,8 @@ int pst_clock_counters(pst_ctx* ctx, uint64_t* out, int32_t reset) {
   if (!ctx) return PST_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  if (out) HIPCHK(hipMemcpy(out, ctx->d_clk, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  if (reset) {
-    HIPCHK(hipMemsetAsync(ctx->d_clk, 0, 6 * sizeof(uint64_t), ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-  }
-  return PST_OK;
+  if (out) HIPCHK(hipMemcpy(out, ctx->d_clk, 24 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return reset ? reset_clock_counters(ctx) : PST_OK;
 }
 
 size_t pst_param_count(int32_t n_levels) {

@@ -1163,6 +1163,215 @@ size_t walk_decoder(const float* base, int D, DecWeights* W) {
 // the same fma chains.
 thread_local bool t_mfma = true;  // set by decode_group for the current call
 
+// ---- fused fold-iteration tail (k_fold_tail): everything between the IPA output projection and
+// the frame update of one structure-module iteration (folding.py:291-455), per 16-node tile, with
+// the activations held in LDS across the chained linears:
+//   act = LN_att(act);  act += tr2(relu(tr1(relu(tr0(act)))));  act = LN_tr(act)   (Transition)
+//   upd = affine_update(act)                                                        (6)
+//   sc  = sc_in(relu(act)) + sc_in1(relu(init_act)); sc += rb2(relu(rb1(relu(sc)))) twice
+//   unnorm = angles(relu(sc))                                                       (6)
+// 11 linears and 2 LayerNorms that ran as 13 launches. The GEMMs run on v_mfma_f32_16x16x4_f32 with
+// D[out channel][node]: A = weight rows W[k][n] (the [in][out] layout every decode Lin has), B =
+// activations from LDS, one fma chain over k ascending per output (plain fp32, no bitwise claim:
+// the decode's tolerance tests hold it to the reference). 8 waves share each GEMM's 16-wide output
+// blocks. LDS activations are stored [node][k & 3][k >> 2] (+4 pad) so a lane reads 4 k-steps of
+// its B operand with one ds_read_b128.
+constexpr int FT_NODES = 16;
+typedef float f32x4t __attribute__((ext_vector_type(4)));
+
+struct FoldTailArgs {
+  float* act;              // [N][384]: in, act after the IPA output projection; out, after LN_tr
+  const float* init_relu;  // [N][128]: relu(initial act)
+  float* upd;              // [N][6]
+  float* unnorm;           // [N][6]
+  int N;
+  const float *att_ln_s, *att_ln_o, *tr_ln_s, *tr_ln_o;
+  const float *w_tr[3], *b_tr[3];
+  const float *w_aff, *b_aff;
+  const float *w_sc, *b_sc, *w_sc1, *b_sc1;
+  const float *w_rb[4], *b_rb[4];  // rb1, rb2, rb1_1, rb2_1
+  const float *w_ang, *b_ang;
+};
+
+// strides of a [16 nodes][C] LDS activation (C = 384 or 128): plane j = k & 3 of node n starts at
+// n * ft_sn(C) + j * ft_sj(C)
+__host__ __device__ constexpr int ft_sj(int C) { return C / 4 + 4; }
+__host__ __device__ constexpr int ft_sn(int C) { return 4 * ft_sj(C); }
+__device__ __forceinline__ int ft_at(int C, int node, int c) { return node * ft_sn(C) + (c & 3) * ft_sj(C) + (c >> 2); }
+
+// acc[b] = X (16 nodes x K, LDS, optional ReLU on load) · W[:, 16·blk_b .. +15], blk_b = b0 + b·bstep
+template <int NB, bool RELU_IN>
+__device__ __forceinline__ void ft_gemm(f32x4t (&acc)[NB], const float* X, int C, int K, const float* __restrict__ W,
+                                        int N, int b0, int bstep, int lane) {
+  const int node = lane & 15, j = lane >> 4;
+  const float* xb = X + node * ft_sn(C) + j * ft_sj(C);
+  int col[NB];
+  bool cv[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    col[b] = 16 * (b0 + b * bstep) + (lane & 15);
+    cv[b] = col[b] < N;
+    acc[b] = f32x4t{0.f, 0.f, 0.f, 0.f};
+  }
+  const int S = K / 4;  // k-steps of 4 (K % 16 == 0)
+  float ac[4][NB], an[4][NB];
+  auto load = [&](float (&a)[4][NB], int s) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) a[u][b] = cv[b] ? W[(int64_t)(4 * (s + u) + j) * N + col[b]] : 0.0f;
+  };
+  load(ac, 0);
+  for (int s = 0; s < S; s += 4) {
+    if (s + 4 < S) load(an, s + 4);
+    f32x4t xv = *reinterpret_cast<const f32x4t*>(xb + s);
+    if (RELU_IN) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xv[u] = xv[u] > 0.0f ? xv[u] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[u][b], xv[u], acc[b], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) ac[u][b] = an[u][b];
+  }
+}
+
+// epilogue into an LDS activation: y = acc + bias (ReLU if RELU_OUT); Y = y, or Y += y (RESID)
+template <int NB, bool RELU_OUT, bool RESID>
+__device__ __forceinline__ void ft_store(const f32x4t (&acc)[NB], float* Y, int C, const float* __restrict__ bias,
+                                         int b0, int bstep, int lane) {
+  const int node = lane & 15;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = 16 * (b0 + b * bstep) + 4 * (lane >> 4) + r;
+      float v = acc[b][r] + bias[n];
+      if (RELU_OUT) v = v > 0.0f ? v : 0.0f;
+      float* y = Y + ft_at(C, node, n);
+      *y = RESID ? *y + v : v;
+    }
+}
+
+// the same epilogue for a 6-wide output (one block, wave 0) straight to global rows [N][6]
+__device__ __forceinline__ void ft_store6(const f32x4t& acc, float* __restrict__ out, const float* __restrict__ bias,
+                                          int64_t node0, int N, int lane) {
+  const int64_t node = node0 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int n = 4 * (lane >> 4) + r;
+    if (n < 6 && node < N) out[node * 6 + n] = acc[r] + bias[n];
+  }
+}
+
+// hk.LayerNorm over the 384 channels of each node, in place in LDS; the operation order of
+// k_layernorm (per-lane sums over c = lane + 64 i in i order, then the xor-shuffle reduction)
+__device__ __forceinline__ void ft_layernorm384(float* X, int node, const float* __restrict__ s,
+                                                const float* __restrict__ o, int lane) {
+  float v[6];
+  float sum = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    v[i] = X[ft_at(384, node, lane + 64 * i)];
+    sum += v[i];
+  }
+  for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
+  const float mean = sum / 384.0f;
+  float sq = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const float d = v[i] - mean;
+    sq += d * d;
+  }
+  for (int m = 32; m >= 1; m >>= 1) sq += __shfl_xor(sq, m);
+  const float rs = 1.0f / sqrtf(sq / 384.0f + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int c = lane + 64 * i;
+    X[ft_at(384, node, c)] = (s[c] * rs) * (v[i] - mean) + o[c];
+  }
+}
+
+__global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
+  __shared__ __attribute__((aligned(16))) float A0[FT_NODES * ft_sn(384)];
+  __shared__ __attribute__((aligned(16))) float T1[FT_NODES * ft_sn(384)];
+  __shared__ __attribute__((aligned(16))) float T2[FT_NODES * ft_sn(384)];
+  __shared__ __attribute__((aligned(16))) float S0[FT_NODES * ft_sn(128)];
+  __shared__ __attribute__((aligned(16))) float S1[FT_NODES * ft_sn(128)];
+  __shared__ __attribute__((aligned(16))) float IR[FT_NODES * ft_sn(128)];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 8 waves
+  const int64_t node0 = (int64_t)blockIdx.x * FT_NODES;
+  // rows in (nodes past N: zeros, never stored)
+  for (int e = threadIdx.x; e < FT_NODES * 384; e += 512) {
+    const int n = e / 384, c = e - 384 * (e / 384);
+    A0[ft_at(384, n, c)] = node0 + n < a.N ? a.act[(node0 + n) * 384 + c] : 0.0f;
+  }
+  for (int e = threadIdx.x; e < FT_NODES * 128; e += 512) {
+    const int n = e >> 7, c = e & 127;
+    IR[ft_at(128, n, c)] = node0 + n < a.N ? a.init_relu[(node0 + n) * 128 + c] : 0.0f;
+  }
+  __syncthreads();
+  ft_layernorm384(A0, 2 * w, a.att_ln_s, a.att_ln_o, lane);
+  ft_layernorm384(A0, 2 * w + 1, a.att_ln_s, a.att_ln_o, lane);
+  __syncthreads();
+  {  // Transition: three 384 x 384 linears, wave w owns output blocks w, w + 8, w + 16
+    f32x4t acc[3];
+    ft_gemm<3, false>(acc, A0, 384, 384, a.w_tr[0], 384, w, 8, lane);
+    ft_store<3, true, false>(acc, T1, 384, a.b_tr[0], w, 8, lane);
+    __syncthreads();
+    ft_gemm<3, false>(acc, T1, 384, 384, a.w_tr[1], 384, w, 8, lane);
+    ft_store<3, true, false>(acc, T2, 384, a.b_tr[1], w, 8, lane);
+    __syncthreads();
+    ft_gemm<3, false>(acc, T2, 384, 384, a.w_tr[2], 384, w, 8, lane);
+    ft_store<3, false, true>(acc, A0, 384, a.b_tr[2], w, 8, lane);  // act += ...
+    __syncthreads();
+  }
+  ft_layernorm384(A0, 2 * w, a.tr_ln_s, a.tr_ln_o, lane);
+  ft_layernorm384(A0, 2 * w + 1, a.tr_ln_s, a.tr_ln_o, lane);
+  __syncthreads();
+  for (int e = threadIdx.x; e < FT_NODES * 384; e += 512) {  // act out (the next iteration's input)
+    const int n = e / 384, c = e - 384 * (e / 384);
+    if (node0 + n < a.N) a.act[(node0 + n) * 384 + c] = A0[ft_at(384, n, c)];
+  }
+  {
+    f32x4t acc[1], acc2[1];
+    if (w == 0) {  // backbone affine update (6 outputs)
+      ft_gemm<1, false>(acc, A0, 384, 384, a.w_aff, 6, 0, 1, lane);
+      ft_store6(acc[0], a.upd, a.b_aff, node0, a.N, lane);
+    }
+    // sidechain input: sc_in(relu(act)) + sc_in1(relu(init_act)), wave w owns block w of 8
+    ft_gemm<1, true>(acc, A0, 384, 384, a.w_sc, 128, w, 1, lane);
+    ft_gemm<1, false>(acc2, IR, 128, 128, a.w_sc1, 128, w, 1, lane);
+    {
+      const int node = lane & 15;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 16 * w + 4 * (lane >> 4) + r;
+        S0[ft_at(128, node, n)] = (acc[0][r] + a.b_sc[n]) + (acc2[0][r] + a.b_sc1[n]);
+      }
+    }
+    __syncthreads();
+    // two residual blocks: sc += rb2(relu(rb1(relu(sc))))
+    for (int rb = 0; rb < 2; ++rb) {
+      ft_gemm<1, true>(acc, S0, 128, 128, a.w_rb[2 * rb], 128, w, 1, lane);
+      ft_store<1, true, false>(acc, S1, 128, a.b_rb[2 * rb], w, 1, lane);
+      __syncthreads();
+      ft_gemm<1, false>(acc, S1, 128, 128, a.w_rb[2 * rb + 1], 128, w, 1, lane);
+      ft_store<1, false, true>(acc, S0, 128, a.b_rb[2 * rb + 1], w, 1, lane);
+      __syncthreads();
+    }
+    if (w == 0) {  // torsion angles (unnormalised, 6 outputs)
+      ft_gemm<1, true>(acc, S0, 128, 128, a.w_ang, 6, 0, 1, lane);
+      ft_store6(acc[0], a.unnorm, a.b_ang, node0, a.N, lane);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_relu_copy(const float* __restrict__ X, int ldx, float* __restrict__ Y,
                                                    int64_t M, int K) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1344,6 +1553,8 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   const int Ni = (int)N;
   const bool fused = !getenv("PST_DECODE_UNFUSED");
   const bool ipa_mfma = !getenv("PST_DECODE_IPA_VALU");  // A/B: the VALU pair sum (same bits)
+  // the fold iteration's tail as one fused launch (PST_DECODE_UNFUSED_TAIL=1: the 13 launches)
+  const bool fold_tail = !getenv("PST_DECODE_UNFUSED_TAIL");
   auto launch = [&]() -> int {
     // ---- upsampler (CrossAttentionScaler, use_original_posenc)
     hipLaunchKernelGGL(k_up_init, dim3((unsigned)T), dim3(128), 0, st, S.tokens, bt, T, dec->d_levels, dec->D,
@@ -1424,6 +1635,14 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
         hipLaunchKernelGGL(k_ipa_local, dim3((unsigned)N), dim3(96), 0, st, S.vpt, S.aff, S.rot, S.feat, Ni);
       }
       gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
+      if (fold_tail) {  // the rest of the iteration's linears and norms in one launch (k_fold_tail)
+        FoldTailArgs ft{S.act, S.init_relu, S.upd, S.unnorm, Ni, W.att_ln.s, W.att_ln.o, W.tr_ln.s, W.tr_ln.o,
+                        {W.tr[0].w, W.tr[1].w, W.tr[2].w}, {W.tr[0].b, W.tr[1].b, W.tr[2].b},
+                        W.affine_update.w, W.affine_update.b, W.sc_in.w, W.sc_in.b, W.sc_in1.w, W.sc_in1.b,
+                        {W.rb1.w, W.rb2.w, W.rb1_1.w, W.rb2_1.w}, {W.rb1.b, W.rb2.b, W.rb1_1.b, W.rb2_1.b},
+                        W.angles.w, W.angles.b};
+        hipLaunchKernelGGL(k_fold_tail, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, ft);
+      } else {
       layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
       gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
       gemm(st, S.tmp384a, 384, W.tr[1], S.tmp384b, 384, Ni, F_RELU_OUT);
@@ -1443,6 +1662,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
       gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
       gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, Ni, F_ACCUM);
       gemm(st, S.sca, 128, W.angles, S.unnorm, 6, Ni, F_RELU_IN);
+      }
       const bool last = it == 7;
       hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.upd, S.unnorm,
                          S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7, last ? S.atom37 : nullptr,
@@ -1461,7 +1681,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     int rc = launch();
     if (rc) return rc;
   } else {
-    std::vector<int64_t> key{(int64_t)t_mfma, (int64_t)fused, (int64_t)ipa_mfma, G.B};
+    std::vector<int64_t> key{(int64_t)t_mfma, (int64_t)fused, (int64_t)ipa_mfma, (int64_t)fold_tail, G.B};
     key.insert(key.end(), G.node_off.begin(), G.node_off.end());
     key.insert(key.end(), G.tok_off.begin(), G.tok_off.end());
     auto it = dec->graphs.find(key);

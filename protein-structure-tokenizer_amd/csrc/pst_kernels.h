@@ -91,8 +91,7 @@ struct MpnnArgs {
   int32_t* q_head;
   int32_t* q_done;
   int64_t q_grid;
-  // clock stamps (measurement): the first wave of workgroup 0 adds its s_memtime (shader clock)
-  // and s_memrealtime (100 MHz) deltas to clk[0], clk[1] (pst_clock_counters); null = off
+  // clock / occupancy stamps (measurement, 8 u64, see ClockStamp and pst_clock_counters); null = off
   unsigned long long* clk;
   // outputs
   float* e_out;  // blocked (null for the last layer)

@@ -69,6 +69,9 @@ __device__ __forceinline__ void make_frame(const double* N, const double* CA, co
   }
 }
 
+// F32: float32 positions (pst_tokenize_f32) — a template parameter, so the coordinate loads carry
+// no per-element branch between the two input formats
+template <bool F32>
 __global__ __launch_bounds__(512) void k_prep(PrepArgs a) {
   __shared__ int wave_cnt[8];
   const int b = a.prot0 + (int)blockIdx.x;
@@ -95,21 +98,38 @@ __global__ __launch_bounds__(512) void k_prep(PrepArgs a) {
     // positions widened to f64 on load: float32 inputs (pst_tokenize_f32) give the same doubles the
     // f64 path reads for float32-exact coordinates, so everything below is bitwise unchanged
     const int64_t p0 = (off + tid) * NATOM * 3;
-    auto P = [&](int i) -> double { return a.pos32 ? (double)a.pos32[p0 + i] : a.pos[p0 + i]; };
+    auto P = [&](int i) -> double { return F32 ? (double)a.pos32[p0 + i] : a.pos[p0 + i]; };
     const uint8_t* fl = a.flags + (off + tid) * NATOM;
     double bb[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) bb[i] = P(i);
     make_frame(bb + 0, bb + 3, bb + 6, a.frame + slot * 9);
+    // centroid over the atoms with gt_exists & atom_exists (preprocessing.py:72), summed in atom
+    // order. The 37 flags are loaded together, then the present atoms' coordinates 8 atoms at a
+    // time (exec-masked loads issued back to back, one wait per group): loading each atom's flag
+    // and then its coordinates made ~37 dependent memory round trips per residue.
+    uint8_t f[NATOM];
+#pragma unroll
+    for (int at = 0; at < NATOM; ++at) f[at] = fl[at];
     double sx = 0.0, sy = 0.0, sz = 0.0;
     int cnt = 0;
-    for (int at = 0; at < NATOM; ++at)
-      if ((fl[at] & 3) == 3) {  // gt_exists & atom_exists (preprocessing.py:72)
-        const double x = P(3 * at), y = P(3 * at + 1), z = P(3 * at + 2);
-        if (cnt == 0) { sx = x; sy = y; sz = z; }
-        else { sx += x; sy += y; sz += z; }
-        ++cnt;
-      }
+    constexpr int CH = 8;
+#pragma unroll
+    for (int a0 = 0; a0 < NATOM; a0 += CH) {
+      double xs[CH][3];
+#pragma unroll
+      for (int k = 0; k < CH; ++k)
+        if (a0 + k < NATOM && (f[a0 + k] & 3) == 3)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) xs[k][c] = P(3 * (a0 + k) + c);
+#pragma unroll
+      for (int k = 0; k < CH; ++k)
+        if (a0 + k < NATOM && (f[a0 + k] & 3) == 3) {
+          if (cnt == 0) { sx = xs[k][0]; sy = xs[k][1]; sz = xs[k][2]; }
+          else { sx += xs[k][0]; sy += xs[k][1]; sz += xs[k][2]; }
+          ++cnt;
+        }
+    }
     a.cen[slot * 3 + 0] = sx / cnt;
     a.cen[slot * 3 + 1] = sy / cnt;
     a.cen[slot * 3 + 2] = sz / cnt;
@@ -765,27 +785,33 @@ __device__ __forceinline__ void mpnn_node_tile(const MpnnArgs& a, int64_t g0, in
   }
 }
 
-// Clock stamps of a fused MPNN launch (measurement, MpnnArgs::clk): the first wave of workgroup 0
-// reads the shader clock counter (s_memtime) and the 100 MHz real-time counter at its start and
-// end and adds both deltas to clk[0..1] (one lane, vector atomics). The clock over the wave's
-// lifetime = d(memtime) / d(memrealtime) x 100 MHz; for the persistent k_mpnn_q that wave lives
-// as long as the launch.
+// Clock stamps of a fused MPNN launch (measurement, MpnnArgs::clk, 8 u64 per layer): the first
+// wave of workgroup 0 adds its s_memtime (shader clock) and s_memrealtime (100 MHz) deltas to
+// clk[0..1] — clock = d(memtime) / d(memrealtime) x 100 MHz, over the launch for the persistent
+// k_mpnn_q whose waves live as long as it does; every wave adds its lifetime (100 MHz ticks) to
+// clk[2], lowers clk[3] to its start, raises clk[4] to its end and counts itself in clk[5], so
+// the launch's wave-slot occupancy is clk[2] / (slots x (clk[4] - clk[3])). One lane, vector
+// atomics, twice per wave.
 struct ClockStamp {
   uint64_t t0 = 0, r0 = 0;
-  bool on = false;
   __device__ __forceinline__ void start(unsigned long long* clk) {
-    on = clk && blockIdx.x == 0 && threadIdx.x < 64;
-    if (on) {
+    if (clk) {
       t0 = __builtin_amdgcn_s_memtime();
       r0 = __builtin_amdgcn_s_memrealtime();
     }
   }
   __device__ __forceinline__ void stop(unsigned long long* clk) {
-    if (on) {
+    if (clk) {
       const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-      if (threadIdx.x == 0) {
-        atomicAdd(clk, (unsigned long long)(t1 - t0));
-        atomicAdd(clk + 1, (unsigned long long)(r1 - r0));
+      if ((threadIdx.x & 63) == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+          atomicAdd(clk, (unsigned long long)(t1 - t0));
+          atomicAdd(clk + 1, (unsigned long long)(r1 - r0));
+        }
+        atomicAdd(clk + 2, (unsigned long long)(r1 - r0));
+        atomicMin(clk + 3, (unsigned long long)r0);
+        atomicMax(clk + 4, (unsigned long long)r1);
+        atomicAdd(clk + 5, 1ull);
       }
     }
   }
@@ -1902,7 +1928,9 @@ __global__ __launch_bounds__(256) void k_table_gemm(const float* __restrict__ X,
 
 // --------------------------------------------------------------------------- launchers
 void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st) {
-  if (n_prot > 0) hipLaunchKernelGGL(k_prep, dim3(n_prot), dim3(512), 0, st, a);
+  if (n_prot <= 0) return;
+  if (a.pos32) hipLaunchKernelGGL(k_prep<true>, dim3(n_prot), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL(k_prep<false>, dim3(n_prot), dim3(512), 0, st, a);
 }
 void launch_knn(const KnnArgs& a, hipStream_t st) {
   if (a.n_slots > a.slot0) hipLaunchKernelGGL(k_knn, dim3((unsigned)((a.n_slots - a.slot0 + 3) / 4)), dim3(256), 0, st, a);

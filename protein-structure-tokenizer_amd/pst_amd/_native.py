@@ -314,9 +314,10 @@ class Tokenizer:
         self._check(lib().pst_sync(self._h))
 
     def clock_counters(self, reset: bool = False) -> np.ndarray:
-        """(shader cycles, 100 MHz ticks) per fused MPNN layer summed since the last reset, uint64
-        [3, 2] (pst_clock_counters); clock of layer l = c[l, 0] / c[l, 1] x 0.1 GHz."""
-        out = np.zeros((3, 2), np.uint64)
+        """Per fused MPNN layer since the last reset, uint64 [3, 8] (pst_clock_counters): shader
+        cycles and 100 MHz ticks of the stamping wave (clock = c[l, 0] / c[l, 1] x 0.1 GHz), Σ wave
+        lifetimes, earliest start, latest end, waves."""
+        out = np.zeros((3, 8), np.uint64)
         self._check(lib().pst_clock_counters(self._h, _ptr(out), 1 if reset else 0))
         return out
 

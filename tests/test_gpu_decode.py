@@ -214,6 +214,36 @@ def test_fused_pair_kernel_matches_library_path(monkeypatch):
         assert np.max(np.abs(a - b)) < 1e-3
 
 
+def test_fused_fold_tail_matches_separate_launches(monkeypatch):
+    """k_fold_tail (the structure module iteration's transition, affine update and sidechain
+    linears + both LayerNorms in one launch per 16-node tile, activations in LDS) against the 13
+    separate launches (PST_DECODE_UNFUSED_TAIL=1): a ragged group of proteins whose node counts are
+    not multiples of 16 (the partial last tile), df 1 and df 4; torsion angles, trajectory and atoms
+    agree to float32 reordering noise (one fma chain over k vs the split-K GEMMs)."""
+    monkeypatch.setenv("PST_DEBUG", "1")
+    from pst_amd._native import Decoder
+    rng = np.random.default_rng(23)
+    for cb, df, lens in ((4096, 1, (37, 96, 5, 131)), (64000, 4, (12, 33))):
+        D = len(LEVELS[cb])
+        toks = [rng.integers(0, cb, n) for n in lens]
+        dec = Decoder(0, cb, df, P.pack_decoder(P.random_full_params(D, 31), D))
+        n_nodes = df * sum(lens)
+        fused = dec.decode(toks)
+        traj_f = dec.debug(2, 8 * n_nodes * 7).copy()
+        ang_f = dec.debug(3, 8 * n_nodes * 6).copy()
+        monkeypatch.setenv("PST_DECODE_UNFUSED_TAIL", "1")
+        ref = dec.decode(toks)
+        traj_r = dec.debug(2, 8 * n_nodes * 7).copy()
+        ang_r = dec.debug(3, 8 * n_nodes * 6).copy()
+        monkeypatch.delenv("PST_DECODE_UNFUSED_TAIL")
+        dec.close()
+        assert np.all(np.isfinite(traj_f)) and np.all(np.isfinite(ang_f))
+        assert np.max(np.abs(ang_f - ang_r)) < 1e-4, (cb, df)
+        assert np.max(np.abs(traj_f - traj_r)) < 1e-3, (cb, df)
+        for a, b in zip(fused, ref):
+            assert np.max(np.abs(a - b)) < 1e-3
+
+
 def test_gemm_mfma_matches_valu_gemm(monkeypatch):
     """The per-node GEMMs run on the in-tree split-K f32-MFMA kernel (k_gemm_mfma, default) or on
     the LDS-tiled VALU kernel (PST_DECODE_NO_MFMA=1, one fma chain over k). The split K changes
