@@ -1296,6 +1296,68 @@ __device__ __forceinline__ void ft_layernorm384(float* X, int node, const float*
   }
 }
 
+// hk.LayerNorm over 128 channels of one node held in LDS ([node][k & 3][k >> 2] layout), written
+// to Y (may be X); k_layernorm's operation order (lane sums c = lane, lane + 64, xor reduction)
+__device__ __forceinline__ void ft_layernorm128(const float* X, float* Y, int node, const float* __restrict__ s,
+                                                const float* __restrict__ o, int lane) {
+  const float v0 = X[ft_at(128, node, lane)], v1 = X[ft_at(128, node, lane + 64)];
+  float sum = 0.0f;
+  sum += v0;
+  sum += v1;
+  for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
+  const float mean = sum / 128.0f;
+  float sq = 0.0f;
+  const float d0 = v0 - mean, d1 = v1 - mean;
+  sq += d0 * d0;
+  sq += d1 * d1;
+  for (int m = 32; m >= 1; m >>= 1) sq += __shfl_xor(sq, m);
+  const float rs = 1.0f / sqrtf(sq / 128.0f + 1e-5f);
+  Y[ft_at(128, node, lane)] = (s[lane] * rs) * d0 + o[lane];
+  Y[ft_at(128, node, lane + 64)] = (s[lane + 64] * rs) * d1 + o[lane + 64];
+}
+
+// The upsampler's Transition on 128-channel rows, fused (modules.py:599-636): x += W2(relu(W1(LN(x))
+// + b1)) + b2, hidden 256, per 16-row tile in LDS (the k_fold_tail machinery); one launch instead
+// of LayerNorm + two GEMMs.
+struct Trans128Args {
+  float* x;  // [M][128], updated in place
+  int M;
+  const float *ln_s, *ln_o, *w1, *b1, *w2, *b2;  // w1 [128][256], w2 [256][128]
+};
+
+__global__ __launch_bounds__(512) void k_transition128(Trans128Args a) {
+  __shared__ __attribute__((aligned(16))) float X[FT_NODES * ft_sn(128)];
+  __shared__ __attribute__((aligned(16))) float Xn[FT_NODES * ft_sn(128)];
+  __shared__ __attribute__((aligned(16))) float Hs[FT_NODES * ft_sn(256)];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t row0 = (int64_t)blockIdx.x * FT_NODES;
+  for (int e = threadIdx.x; e < FT_NODES * 128; e += 512) {
+    const int n = e >> 7, c = e & 127;
+    X[ft_at(128, n, c)] = row0 + n < a.M ? a.x[(row0 + n) * 128 + c] : 0.0f;
+  }
+  __syncthreads();
+  ft_layernorm128(X, Xn, 2 * w, a.ln_s, a.ln_o, lane);
+  ft_layernorm128(X, Xn, 2 * w + 1, a.ln_s, a.ln_o, lane);
+  __syncthreads();
+  {
+    f32x4t acc[2];
+    ft_gemm<2, false>(acc, Xn, 128, 128, a.w1, 256, w, 8, lane);
+    ft_store<2, true, false>(acc, Hs, 256, a.b1, w, 8, lane);
+  }
+  __syncthreads();
+  {
+    f32x4t acc[1];
+    ft_gemm<1, false>(acc, Hs, 256, 256, a.w2, 128, w, 1, lane);
+    ft_store<1, false, true>(acc, X, 128, a.b2, w, 1, lane);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < FT_NODES * 128; e += 512) {
+    const int n = e >> 7, c = e & 127;
+    if (row0 + n < a.M) a.x[(row0 + n) * 128 + c] = X[ft_at(128, n, c)];
+  }
+}
+
 __global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
   __shared__ __attribute__((aligned(16))) float A0[FT_NODES * ft_sn(384)];
   __shared__ __attribute__((aligned(16))) float T1[FT_NODES * ft_sn(384)];
@@ -1570,12 +1632,19 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
       gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, (int)T, 0);
       hipLaunchKernelGGL(k_up_attn, dim3((unsigned)N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, bt, N);
       gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, Ni, F_ACCUM);
+      if (fold_tail) {  // the two Transitions fused (k_transition128), same gating as k_fold_tail
+        Trans128Args ta{S.res, Ni, W.rt_ln[b].s, W.rt_ln[b].o, W.rt1[b].w, W.rt1[b].b, W.rt2[b].w, W.rt2[b].b};
+        hipLaunchKernelGGL(k_transition128, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, ta);
+        Trans128Args tb{S.orig, (int)T, W.ot_ln[b].s, W.ot_ln[b].o, W.ot1[b].w, W.ot1[b].b, W.ot2[b].w, W.ot2[b].b};
+        hipLaunchKernelGGL(k_transition128, dim3((unsigned)((T + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, tb);
+      } else {
       layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.rt_ln[b]);
       gemm(st, S.ln_a, 128, W.rt1[b], S.tr_h, 256, Ni, F_RELU_OUT);
       gemm(st, S.tr_h, 256, W.rt2[b], S.res, 128, Ni, F_ACCUM);
       layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.ot_ln[b]);
       gemm(st, S.ln_b, 128, W.ot1[b], S.tr_h, 256, (int)T, F_RELU_OUT);
       gemm(st, S.tr_h, 256, W.ot2[b], S.orig, 128, (int)T, F_ACCUM);
+      }
     }
     hipLaunchKernelGGL(k_spherical, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.res, Ni);  // s_i
     // ---- sequence decoder: pair representation over each protein's N_b² pairs
