@@ -1358,6 +1358,55 @@ __global__ __launch_bounds__(512) void k_transition128(Trans128Args a) {
   }
 }
 
+// LayerNorm of 128-channel rows and two 128 -> 128 projections of the normalised rows, fused (the
+// upsampler's query / gate and key / value inputs, modules.py:537-598): y_i = f_i(LN(x)·W_i + b_i)
+// with f = identity, × key_dim^-0.5 (F_QSCALE) or sigmoid (F_SIGMOID_OUT); b_i may be null. One
+// launch instead of a LayerNorm and two GEMMs.
+struct LnProj2Args {
+  const float* x;  // [M][128]
+  int M;
+  const float *ln_s, *ln_o;
+  const float *w[2], *b[2];
+  int flags[2];
+  float* y[2];  // [M][128] each
+};
+
+__global__ __launch_bounds__(512) void k_ln_proj2(LnProj2Args a) {
+  __shared__ __attribute__((aligned(16))) float X[FT_NODES * ft_sn(128)];
+  __shared__ __attribute__((aligned(16))) float Y[2][FT_NODES * ft_sn(128)];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t row0 = (int64_t)blockIdx.x * FT_NODES;
+  for (int e = threadIdx.x; e < FT_NODES * 128; e += 512) {
+    const int n = e >> 7, c = e & 127;
+    X[ft_at(128, n, c)] = row0 + n < a.M ? a.x[(row0 + n) * 128 + c] : 0.0f;
+  }
+  __syncthreads();
+  ft_layernorm128(X, X, 2 * w, a.ln_s, a.ln_o, lane);
+  ft_layernorm128(X, X, 2 * w + 1, a.ln_s, a.ln_o, lane);
+  __syncthreads();
+  for (int p = 0; p < 2; ++p) {  // wave w: output block w of both projections
+    f32x4t acc[1];
+    ft_gemm<1, false>(acc, X, 128, 128, a.w[p], 128, w, 1, lane);
+    const int node = lane & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = 16 * w + 4 * (lane >> 4) + r;
+      float v = acc[0][r];
+      if (a.b[p]) v = v + a.b[p][n];
+      if (a.flags[p] & F_SIGMOID_OUT) v = 1.0f / (1.0f + expf(-v));
+      if (a.flags[p] & F_QSCALE) v = v * Q_SCALE;
+      Y[p][ft_at(128, node, n)] = v;
+    }
+  }
+  __syncthreads();
+  for (int p = 0; p < 2; ++p)
+    for (int e = threadIdx.x; e < FT_NODES * 128; e += 512) {
+      const int n = e >> 7, c = e & 127;
+      if (row0 + n < a.M) a.y[p][(row0 + n) * 128 + c] = Y[p][ft_at(128, n, c)];
+    }
+}
+
 __global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
   __shared__ __attribute__((aligned(16))) float A0[FT_NODES * ft_sn(384)];
   __shared__ __attribute__((aligned(16))) float T1[FT_NODES * ft_sn(384)];
@@ -1624,12 +1673,21 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     gemm(st, S.orig_in, 256, W.proj_original, S.orig, 128, (int)T, 0);
     hipLaunchKernelGGL(k_node_pe, dim3((unsigned)N), dim3(128), 0, st, dec->d_pe_node, bt, N, S.res);
     for (int b = 0; b < 3; ++b) {
+      if (fold_tail) {  // LayerNorm + both projections per operand in one launch (k_ln_proj2)
+        LnProj2Args qa{S.res, Ni, W.qn[b].s, W.qn[b].o, {W.wq[b], W.wg[b]}, {nullptr, W.gb[b]},
+                       {F_QSCALE, F_SIGMOID_OUT}, {S.q, S.gate}};
+        hipLaunchKernelGGL(k_ln_proj2, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, qa);
+        LnProj2Args ka{S.orig, (int)T, W.dn[b].s, W.dn[b].o, {W.wk[b], W.wv[b]}, {nullptr, nullptr}, {0, 0},
+                       {S.k, S.v}};
+        hipLaunchKernelGGL(k_ln_proj2, dim3((unsigned)((T + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, ka);
+      } else {
       layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.qn[b]);
       layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.dn[b]);
       gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, Ni, F_QSCALE);  // q · key_dim^-0.5
       gemm_raw(st, S.ln_a, 128, W.wg[b], 128, 128, W.gb[b], S.gate, 128, Ni, F_SIGMOID_OUT);
       gemm_raw(st, S.ln_b, 128, W.wk[b], 128, 128, nullptr, S.k, 128, (int)T, 0);
       gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, (int)T, 0);
+      }
       hipLaunchKernelGGL(k_up_attn, dim3((unsigned)N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, bt, N);
       gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, Ni, F_ACCUM);
       if (fold_tail) {  // the two Transitions fused (k_transition128), same gating as k_fold_tail
