@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <cerrno>
 #include <functional>
 #include <string>
@@ -471,30 +472,35 @@ int run_pool(int32_t n, int32_t n_threads, const std::function<size_t(int)>& siz
 // Chunk size of pass 1: a 320 KB PDB file (the largest CASP14 one) splits into ~7 chunks
 constexpr size_t kScanChunk = 48 << 10;
 
-// Both passes over the n texts of a batch (items already marked failed are skipped): pass 1 over
-// all chunks of all texts at once, then pass 2 per text, each on the thread pool
+// Both passes over the n texts of a batch (items already marked failed are skipped) in ONE pool
+// job: the tasks are the pass-1 chunks of all texts, largest text first; the worker that scans the
+// LAST chunk of a text runs that text's pass 2 right away. A text's pass 2 (sequential, Bio's
+// order) therefore overlaps the other texts' pass 1 instead of waiting for every chunk of the batch
+// (two pool jobs before: the largest file's pass 2 ran after all of pass 1, on one thread).
 void parse_texts(int32_t n, const char* const* texts, const size_t* lens, char chain_id, int32_t n_threads,
                  std::vector<Parsed>& items) {
   std::vector<std::vector<size_t>> starts(n);
   std::vector<std::vector<std::vector<Rec>>> recs(n);
   std::vector<std::pair<int, int>> tasks;
-  for (int32_t i = 0; i < n; ++i) {
-    if (items[i].status != PST_OK) continue;
+  std::vector<int> order;
+  for (int32_t i = 0; i < n; ++i)
+    if (items[i].status == PST_OK) order.push_back(i);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lens[a] > lens[b]; });
+  std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[std::max(1, n)]);
+  for (int i : order) {
     starts[i] = chunk_starts(texts[i], lens[i], kScanChunk);
     recs[i].resize(starts[i].size());
+    left[i].store((int)starts[i].size());
     for (int c = 0; c < (int)starts[i].size(); ++c) tasks.emplace_back(i, c);
   }
   auto chunk_end = [&](int i, int c) { return c + 1 < (int)starts[i].size() ? starts[i][c + 1] : lens[i]; };
-  run_pool((int32_t)tasks.size(), n_threads,
-           [&](int t) { return chunk_end(tasks[t].first, tasks[t].second) - starts[tasks[t].first][tasks[t].second]; },
-           [&](int t) {
-             const int i = tasks[t].first, c = tasks[t].second;
-             scan_chunk(texts[i], lens[i], starts[i][c], chunk_end(i, c), &recs[i][c]);
-           });
-  run_pool(n, n_threads, [&](int i) { return lens[i]; }, [&](int i) {
-    if (items[i].status != PST_OK) return;
-    assemble(texts[i], lens[i], recs[i], chain_id, &items[i]);
-    std::vector<std::vector<Rec>>().swap(recs[i]);
+  pst::HostPool::get().run((int32_t)tasks.size(), n_threads > 0 ? n_threads : 1, [&](int t) {
+    const int i = tasks[t].first, c = tasks[t].second;
+    scan_chunk(texts[i], lens[i], starts[i][c], chunk_end(i, c), &recs[i][c]);
+    if (left[i].fetch_sub(1, std::memory_order_acq_rel) == 1) {  // this text's last chunk: pass 2
+      assemble(texts[i], lens[i], recs[i], chain_id, &items[i]);
+      std::vector<std::vector<Rec>>().swap(recs[i]);
+    }
   });
 }
 
