@@ -478,7 +478,8 @@ __device__ __forceinline__ void tile_gemm_mix_f(Tile& acc, const Tile& X, const 
       // the global stream starts GEMM_DEPTH k-steps before the LDS part ends
       if (t == KL - GEMM_DEPTH) {
 #pragma unroll
-        for (int i = 0; i < GEMM_DEPTH; ++i) ring[i] = buf_load4(rs, vo, (KL + i) * 1024);
+        for (int i = 0; i < GEMM_DEPTH; ++i)
+          if (KL + i < 64) ring[i] = buf_load4(rs, vo, (KL + i) * 1024);
       }
       if (g < 64 / G - 1 && (j & 1) == 0) {
         const int u = t + G;

@@ -91,6 +91,7 @@ struct MpnnArgs {
   int32_t* q_head;
   int32_t* q_done;
   int64_t q_grid;
+  int32_t q_waves;  // 4 or 8 waves per queue workgroup (k_mpnn_q<L, NW>)
   // clock / occupancy stamps (measurement, 8 u64, see ClockStamp and pst_clock_counters); null = off
   unsigned long long* clk;
   // outputs

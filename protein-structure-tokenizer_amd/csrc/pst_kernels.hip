@@ -552,7 +552,7 @@ __device__ __forceinline__ int32_t edge_sender(const MpnnArgs& a, int64_t g0, in
 #ifndef E_STORE_SPREAD
 #define E_STORE_SPREAD 1
 #endif
-template <int LAYER>
+template <int LAYER, int KL = w1_lds_ksteps<LAYER>()>
 __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int64_t g0, int lane, int blk,
                                            int32_t s_pre, Tile& m, const float4* w1_lds = nullptr) {
   const int te = 32 * blk + (lane & 31);
@@ -605,14 +605,14 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
       feat_gemm_st<true>(m, x, a.W_msg0f, &e, make_rsrc_or_null(a.e_out ? a.e_out + eblk : nullptr));
     else
       feat_gemm(m, x, a.W_msg0f);
-    msg_hidden<w1_lds_ksteps<LAYER>()>(m, a.msg, w1_lds);
+    msg_hidden<KL>(m, a.msg, w1_lds);
   } else {
     tile_add_rows(m, a.P_in + s * 512 + 256, a.P_in + g * 512 + 384);
     if (E_STORE_SPREAD)  // e leaves during the GEMM that reads it (tile_gemm_store)
       tile_gemm_store(m, e, a.msg.w0, make_rsrc_or_null(a.e_out ? a.e_out + eblk : nullptr));
     else
       tile_gemm(m, e, a.msg.w0);
-    msg_hidden<w1_lds_ksteps<LAYER>()>(m, a.msg, w1_lds);
+    msg_hidden<KL>(m, a.msg, w1_lds);
   }
 }
 
@@ -671,9 +671,9 @@ __device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, 
 // The edge phase of one fused-layer task (receivers task*32 .. task*32+31), edge blocks blk_lo ..
 // blk_hi-1 in order: edge update / embedding, message MLP, and the ordered segment sums of the
 // receivers these blocks complete, stored to agg (perm rows). lds_scratch[w]: this wave's LDS tile.
-template <int LAYER>
+template <int LAYER, int KL, int NW>
 __device__ __forceinline__ void mpnn_edge_blocks(const MpnnArgs& a, int64_t task, int lane, int blk_lo, int blk_hi,
-                                                 const float4* w1_lds, float (&lds_scratch)[4][64 * 36], int w) {
+                                                 const float4* w1_lds, float (&lds_scratch)[NW][64 * 36], int w) {
   const int64_t g0 = task * 32;
   float* scratch = lds_scratch[w];
   float* aggl = a.agg + task * 32 * 128;
@@ -684,7 +684,7 @@ __device__ __forceinline__ void mpnn_edge_blocks(const MpnnArgs& a, int64_t task
     const int32_t s_cur = s_next;
     if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
-    edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m, w1_lds);
+    edge_block<LAYER, KL>(a, task, g0, lane, blk, s_cur, m, w1_lds);
     // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order). The
     // block holds edges of two receivers: rA (block edges 0..lastA) and rA+1 (the rest).
     // Transpose through LDS two accumulator blocks at a time, so that lane l owns channel
@@ -991,19 +991,22 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 // loop (carried, they spilled 43 VGPRs and 149 SGPRs).
 typedef const MpnnArgs __attribute__((address_space(4)))* MpnnArgsK;
 
-template <int LAYER>
-__global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_q(MpnnArgs a_in) {
+// NW: waves per workgroup — 4 (two workgroups per CU, the first w1_lds_ksteps k-steps of W1 in
+// LDS) or 8 (one workgroup per CU sharing ALL 64 W1 k-steps through LDS: a persistent grid has no
+// tail for the larger workgroup to lengthen)
+template <int LAYER, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void k_mpnn_q(MpnnArgs a_in) {
   const MpnnArgsK a_k = (MpnnArgsK)__builtin_amdgcn_kernarg_segment_ptr();
   ClockStamp cs;
   cs.start(a_in.clk);
-  __shared__ float lds_scratch[4][64 * 36];
+  __shared__ float lds_scratch[NW][64 * 36];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr int KL = w1_lds_ksteps<LAYER>();
+  constexpr int KL = NW == 8 ? 64 : w1_lds_ksteps<LAYER>();
   __shared__ float4 w1_lds_buf[(KL > 0 ? KL : 1) * 64];
   const float4* w1_lds = KL > 0 ? w1_lds_buf : nullptr;
   if (KL > 0) {
-    for (int i = threadIdx.x; i < KL * 64; i += 256) w1_lds_buf[i] = a_k->msg.w1[i];
+    for (int i = threadIdx.x; i < KL * 64; i += 64 * NW) w1_lds_buf[i] = a_k->msg.w1[i];
     __syncthreads();
   }
   // HW_REG_XCC_ID (hwreg 20): bits 0-3 = this wave's XCD
@@ -1024,7 +1027,7 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn_q(MpnnArgs a_in) 
     }
     const int64_t task = t0 + (j >> 1);
     const int hh = j & 1;
-    mpnn_edge_blocks<LAYER>(a, task, lane, 25 * hh, 25 * hh + 25, w1_lds, lds_scratch, w);
+    mpnn_edge_blocks<LAYER, KL, NW>(a, task, lane, 25 * hh, 25 * hh + 25, w1_lds, lds_scratch, w);
     // hand-off of this half's segment sums: stores drained, agent release, then the counter
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1956,10 +1959,17 @@ void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st) {
   }
   if (a.q_head) {  // persistent half-task queue: every wave slot, at most one unit per wave
     const int64_t units = 2 * a.n_tasks;
+    if (a.q_waves == 8) {  // q_grid counts 4-wave workgroups: half as many 8-wave ones
+      const dim3 qgrid((unsigned)std::min<int64_t>((units + 7) / 8, a.q_grid / 2));
+      if (layer == 0) hipLaunchKernelGGL((k_mpnn_q<0, 8>), qgrid, dim3(512), 0, st, a);
+      else if (layer == 1) hipLaunchKernelGGL((k_mpnn_q<1, 8>), qgrid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((k_mpnn_q<2, 8>), qgrid, dim3(512), 0, st, a);
+      return;
+    }
     const dim3 qgrid((unsigned)std::min<int64_t>((units + 3) / 4, a.q_grid));
-    if (layer == 0) hipLaunchKernelGGL(k_mpnn_q<0>, qgrid, dim3(256), 0, st, a);
-    else if (layer == 1) hipLaunchKernelGGL(k_mpnn_q<1>, qgrid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_mpnn_q<2>, qgrid, dim3(256), 0, st, a);
+    if (layer == 0) hipLaunchKernelGGL((k_mpnn_q<0, 4>), qgrid, dim3(256), 0, st, a);
+    else if (layer == 1) hipLaunchKernelGGL((k_mpnn_q<1, 4>), qgrid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_mpnn_q<2, 4>), qgrid, dim3(256), 0, st, a);
     return;
   }
   if (a.half_tasks) {  // two waves per task (n_tasks % 4 == 0: run() pads slots to 128)

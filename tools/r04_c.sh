@@ -19,5 +19,7 @@ for r in 1 2; do
 done
 unset PST_DECODE_UNFUSED_TAIL
 echo decode ok
+timeout -k 10 500 bash tools/env_ab.sh 1024 - PST_MPNN_QWAVES=8 - PST_MPNN_QWAVES=8 > gpurun_out/${TAG}_qwaves.txt 2>&1
+echo qwaves ok
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e > gpurun_out/${TAG}_prof.log 2>&1
 echo done
