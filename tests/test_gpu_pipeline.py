@@ -166,9 +166,12 @@ def test_two_proteins_small_first():
 
 def test_clock_counters_accumulate_and_reset():
     """pst_clock_counters (bench.py's clock fields): each fused MPNN launch's stamping wave adds
-    (shader cycles, 100 MHz ticks); two calls add about twice one call's ticks, reset zeroes them,
-    the implied clock is a plausible gfx950 shader clock, and the tokens are unaffected."""
+    (shader cycles, 100 MHz ticks) and every wave its lifetime; two calls add about twice one call's
+    ticks, reset restarts them, the implied clock is a plausible gfx950 shader clock, the queue
+    form's wave-slot occupancy is high (one launch per layer: one chunk), and the tokens are
+    unaffected."""
     from pst_amd._native import Tokenizer
+    os.environ["PST_H2D_CHUNKS"] = "1"  # one k_mpnn_q launch per layer per call
     samples = synthetic.synthetic_batch(512, 256, seed=1000)  # fused layers (queue form)
     pos, flags, off = pack_samples(samples)
     t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
