@@ -250,7 +250,8 @@ struct pst_ctx {
   int32_t* h_counts = nullptr;  // pinned host copy of [n_tok | n_nodes] (cap_B each)
   int32_t last_down_form = 0;  // pst::DOWN_* of the last run (pst_debug_fetch 20, plan[19])
   int64_t half_tasks = -2;   // PST_HALF_TASKS: 1 = fused layers always two waves per task, 0 = never; -1 = policy
-  int64_t mpnn_qwaves = -2;  // PST_MPNN_QWAVES: 8 = one 8-wave queue workgroup per CU (all of W1 in LDS); else 4
+  int64_t mpnn_qwaves = -2;  // PST_MPNN_QWAVES: 4 = two 4-wave queue workgroups per CU; else one 8-wave workgroup
+                             // per CU with all of W1 in LDS (k_mpnn<0..2> -1.0..-2.8 %, profiles/r04_ab_qwaves.txt)
   int64_t mpnn_queue = -2;   // PST_MPNN_QUEUE: 1 = fused layers as the half-task queue (k_mpnn_q) whenever not
                              // k_mpnn<L, true>, 0 = never (k_mpnn<L, false>); -1 = policy
   std::vector<int64_t> h_offsets;
@@ -678,7 +679,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
       m.q_done = m.q_head + 128;
       m.q_grid = 2 * (ctx->n_simds / 4);  // two 4-wave workgroups per CU (MPNN_MIN_BLOCKS)
       env_threshold(ctx->mpnn_qwaves, "PST_MPNN_QWAVES");
-      m.q_waves = ctx->mpnn_qwaves == 8 ? 8 : 4;
+      m.q_waves = ctx->mpnn_qwaves == 4 ? 4 : 8;
     }
     m.senders = w.senders;
     m.deg = w.deg;

@@ -1199,12 +1199,15 @@ __host__ __device__ constexpr int ft_sj(int C) { return C / 4 + 4; }
 __host__ __device__ constexpr int ft_sn(int C) { return 4 * ft_sj(C); }
 __device__ __forceinline__ int ft_at(int C, int node, int c) { return node * ft_sn(C) + (c & 3) * ft_sj(C) + (c >> 2); }
 
-// acc[b] = X (16 nodes x K, LDS, optional ReLU on load) · W[:, 16·blk_b .. +15], blk_b = b0 + b·bstep
-template <int NB, bool RELU_IN>
-__device__ __forceinline__ void ft_gemm(f32x4t (&acc)[NB], const float* X, int C, int K, const float* __restrict__ W,
-                                        int N, int b0, int bstep, int lane) {
+// acc[b] = X (16 nodes x K, LDS, optional ReLU on load) · W[:, 16·blk_b .. +15], blk_b = b0 + b·bstep.
+// Fully unrolled over K; the weight operands run PF groups of 4 k-steps (16 k) ahead in a register
+// ring (the weights are L2-resident: a fetch is ~1 us, ~4 groups of this wave's MFMAs).
+template <int NB, bool RELU_IN, int K>
+__device__ __forceinline__ void ft_gemm(f32x4t (&acc)[NB], const float* X, const float* __restrict__ W, int N,
+                                        int b0, int bstep, int lane) {
+  constexpr int G = K / 16, PF = G < 4 ? G : 4;
   const int node = lane & 15, j = lane >> 4;
-  const float* xb = X + node * ft_sn(C) + j * ft_sj(C);
+  const float* xb = X + node * ft_sn(K) + j * ft_sj(K);
   int col[NB];
   bool cv[NB];
 #pragma unroll
@@ -1213,18 +1216,18 @@ __device__ __forceinline__ void ft_gemm(f32x4t (&acc)[NB], const float* X, int C
     cv[b] = col[b] < N;
     acc[b] = f32x4t{0.f, 0.f, 0.f, 0.f};
   }
-  const int S = K / 4;  // k-steps of 4 (K % 16 == 0)
-  float ac[4][NB], an[4][NB];
-  auto load = [&](float (&a)[4][NB], int s) {
+  float ring[PF][4][NB];
+  auto load = [&](float (&a)[4][NB], int g) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) a[u][b] = cv[b] ? W[(int64_t)(4 * (s + u) + j) * N + col[b]] : 0.0f;
+      for (int b = 0; b < NB; ++b) a[u][b] = cv[b] ? W[(int64_t)(4 * (4 * g + u) + j) * N + col[b]] : 0.0f;
   };
-  load(ac, 0);
-  for (int s = 0; s < S; s += 4) {
-    if (s + 4 < S) load(an, s + 4);
-    f32x4t xv = *reinterpret_cast<const f32x4t*>(xb + s);
+#pragma unroll
+  for (int p = 0; p < PF; ++p) load(ring[p], p);
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    f32x4t xv = *reinterpret_cast<const f32x4t*>(xb + 4 * g);
     if (RELU_IN) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) xv[u] = xv[u] > 0.0f ? xv[u] : 0.0f;
@@ -1232,11 +1235,8 @@ __device__ __forceinline__ void ft_gemm(f32x4t (&acc)[NB], const float* X, int C
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[u][b], xv[u], acc[b], 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int b = 0; b < NB; ++b) ac[u][b] = an[u][b];
+      for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(ring[g % PF][u][b], xv[u], acc[b], 0, 0, 0);
+    if (g + PF < G) load(ring[g % PF], g + PF);
   }
 }
 
@@ -1342,13 +1342,13 @@ __global__ __launch_bounds__(512) void k_transition128(Trans128Args a) {
   __syncthreads();
   {
     f32x4t acc[2];
-    ft_gemm<2, false>(acc, Xn, 128, 128, a.w1, 256, w, 8, lane);
+    ft_gemm<2, false, 128>(acc, Xn, a.w1, 256, w, 8, lane);
     ft_store<2, true, false>(acc, Hs, 256, a.b1, w, 8, lane);
   }
   __syncthreads();
   {
     f32x4t acc[1];
-    ft_gemm<1, false>(acc, Hs, 256, 256, a.w2, 128, w, 1, lane);
+    ft_gemm<1, false, 256>(acc, Hs, a.w2, 128, w, 1, lane);
     ft_store<1, false, true>(acc, X, 128, a.b2, w, 1, lane);
   }
   __syncthreads();
@@ -1387,7 +1387,7 @@ __global__ __launch_bounds__(512) void k_ln_proj2(LnProj2Args a) {
   __syncthreads();
   for (int p = 0; p < 2; ++p) {  // wave w: output block w of both projections
     f32x4t acc[1];
-    ft_gemm<1, false>(acc, X, 128, 128, a.w[p], 128, w, 1, lane);
+    ft_gemm<1, false, 128>(acc, X, a.w[p], 128, w, 1, lane);
     const int node = lane & 15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1432,13 +1432,13 @@ __global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
   __syncthreads();
   {  // Transition: three 384 x 384 linears, wave w owns output blocks w, w + 8, w + 16
     f32x4t acc[3];
-    ft_gemm<3, false>(acc, A0, 384, 384, a.w_tr[0], 384, w, 8, lane);
+    ft_gemm<3, false, 384>(acc, A0, a.w_tr[0], 384, w, 8, lane);
     ft_store<3, true, false>(acc, T1, 384, a.b_tr[0], w, 8, lane);
     __syncthreads();
-    ft_gemm<3, false>(acc, T1, 384, 384, a.w_tr[1], 384, w, 8, lane);
+    ft_gemm<3, false, 384>(acc, T1, a.w_tr[1], 384, w, 8, lane);
     ft_store<3, true, false>(acc, T2, 384, a.b_tr[1], w, 8, lane);
     __syncthreads();
-    ft_gemm<3, false>(acc, T2, 384, 384, a.w_tr[2], 384, w, 8, lane);
+    ft_gemm<3, false, 384>(acc, T2, a.w_tr[2], 384, w, 8, lane);
     ft_store<3, false, true>(acc, A0, 384, a.b_tr[2], w, 8, lane);  // act += ...
     __syncthreads();
   }
@@ -1452,12 +1452,12 @@ __global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
   {
     f32x4t acc[1], acc2[1];
     if (w == 0) {  // backbone affine update (6 outputs)
-      ft_gemm<1, false>(acc, A0, 384, 384, a.w_aff, 6, 0, 1, lane);
+      ft_gemm<1, false, 384>(acc, A0, a.w_aff, 6, 0, 1, lane);
       ft_store6(acc[0], a.upd, a.b_aff, node0, a.N, lane);
     }
     // sidechain input: sc_in(relu(act)) + sc_in1(relu(init_act)), wave w owns block w of 8
-    ft_gemm<1, true>(acc, A0, 384, 384, a.w_sc, 128, w, 1, lane);
-    ft_gemm<1, false>(acc2, IR, 128, 128, a.w_sc1, 128, w, 1, lane);
+    ft_gemm<1, true, 384>(acc, A0, a.w_sc, 128, w, 1, lane);
+    ft_gemm<1, false, 128>(acc2, IR, a.w_sc1, 128, w, 1, lane);
     {
       const int node = lane & 15;
 #pragma unroll
@@ -1469,15 +1469,15 @@ __global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
     __syncthreads();
     // two residual blocks: sc += rb2(relu(rb1(relu(sc))))
     for (int rb = 0; rb < 2; ++rb) {
-      ft_gemm<1, true>(acc, S0, 128, 128, a.w_rb[2 * rb], 128, w, 1, lane);
+      ft_gemm<1, true, 128>(acc, S0, a.w_rb[2 * rb], 128, w, 1, lane);
       ft_store<1, true, false>(acc, S1, 128, a.b_rb[2 * rb], w, 1, lane);
       __syncthreads();
-      ft_gemm<1, false>(acc, S1, 128, 128, a.w_rb[2 * rb + 1], 128, w, 1, lane);
+      ft_gemm<1, false, 128>(acc, S1, a.w_rb[2 * rb + 1], 128, w, 1, lane);
       ft_store<1, false, true>(acc, S0, 128, a.b_rb[2 * rb + 1], w, 1, lane);
       __syncthreads();
     }
     if (w == 0) {  // torsion angles (unnormalised, 6 outputs)
-      ft_gemm<1, true>(acc, S0, 128, 128, a.w_ang, 6, 0, 1, lane);
+      ft_gemm<1, true, 128>(acc, S0, a.w_ang, 6, 0, 1, lane);
       ft_store6(acc[0], a.unnorm, a.b_ang, node0, a.N, lane);
     }
   }
