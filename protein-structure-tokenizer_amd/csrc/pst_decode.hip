@@ -1056,6 +1056,8 @@ struct pst_decoder {
   // pinned staging of a group's index arrays (one H2D copy per group) and the event of its copy
   char* h_up = nullptr;
   size_t h_up_bytes = 0;
+  float* h_atoms = nullptr;  // pinned staging of a group's atom37 output (D2H at full rate)
+  size_t h_atoms_floats = 0;
   hipEvent_t up_ev = nullptr;
   // decode_group's kernel sequence as HIP graphs, keyed by the group's shape (decode_group)
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
@@ -1407,7 +1409,9 @@ __global__ __launch_bounds__(512) void k_ln_proj2(LnProj2Args a) {
     }
 }
 
-__global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
+// 12 waves: the 384-wide linears' 24 output blocks two per wave; the 128-wide ones on waves 0-7
+constexpr int FT_WAVES = 12;
+__global__ __launch_bounds__(64 * FT_WAVES) void k_fold_tail(FoldTailArgs a) {
   __shared__ __attribute__((aligned(16))) float A0[FT_NODES * ft_sn(384)];
   __shared__ __attribute__((aligned(16))) float T1[FT_NODES * ft_sn(384)];
   __shared__ __attribute__((aligned(16))) float T2[FT_NODES * ft_sn(384)];
@@ -1415,50 +1419,48 @@ __global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
   __shared__ __attribute__((aligned(16))) float S1[FT_NODES * ft_sn(128)];
   __shared__ __attribute__((aligned(16))) float IR[FT_NODES * ft_sn(128)];
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 8 waves
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // FT_WAVES waves
   const int64_t node0 = (int64_t)blockIdx.x * FT_NODES;
   // rows in (nodes past N: zeros, never stored)
-  for (int e = threadIdx.x; e < FT_NODES * 384; e += 512) {
+  for (int e = threadIdx.x; e < FT_NODES * 384; e += 64 * FT_WAVES) {
     const int n = e / 384, c = e - 384 * (e / 384);
     A0[ft_at(384, n, c)] = node0 + n < a.N ? a.act[(node0 + n) * 384 + c] : 0.0f;
   }
-  for (int e = threadIdx.x; e < FT_NODES * 128; e += 512) {
+  for (int e = threadIdx.x; e < FT_NODES * 128; e += 64 * FT_WAVES) {
     const int n = e >> 7, c = e & 127;
     IR[ft_at(128, n, c)] = node0 + n < a.N ? a.init_relu[(node0 + n) * 128 + c] : 0.0f;
   }
   __syncthreads();
-  ft_layernorm384(A0, 2 * w, a.att_ln_s, a.att_ln_o, lane);
-  ft_layernorm384(A0, 2 * w + 1, a.att_ln_s, a.att_ln_o, lane);
+  for (int nd = w; nd < FT_NODES; nd += FT_WAVES) ft_layernorm384(A0, nd, a.att_ln_s, a.att_ln_o, lane);
   __syncthreads();
-  {  // Transition: three 384 x 384 linears, wave w owns output blocks w, w + 8, w + 16
-    f32x4t acc[3];
-    ft_gemm<3, false, 384>(acc, A0, a.w_tr[0], 384, w, 8, lane);
-    ft_store<3, true, false>(acc, T1, 384, a.b_tr[0], w, 8, lane);
+  {  // Transition: three 384 x 384 linears, wave w owns output blocks w, w + 12
+    f32x4t acc[2];
+    ft_gemm<2, false, 384>(acc, A0, a.w_tr[0], 384, w, FT_WAVES, lane);
+    ft_store<2, true, false>(acc, T1, 384, a.b_tr[0], w, FT_WAVES, lane);
     __syncthreads();
-    ft_gemm<3, false, 384>(acc, T1, a.w_tr[1], 384, w, 8, lane);
-    ft_store<3, true, false>(acc, T2, 384, a.b_tr[1], w, 8, lane);
+    ft_gemm<2, false, 384>(acc, T1, a.w_tr[1], 384, w, FT_WAVES, lane);
+    ft_store<2, true, false>(acc, T2, 384, a.b_tr[1], w, FT_WAVES, lane);
     __syncthreads();
-    ft_gemm<3, false, 384>(acc, T2, a.w_tr[2], 384, w, 8, lane);
-    ft_store<3, false, true>(acc, A0, 384, a.b_tr[2], w, 8, lane);  // act += ...
+    ft_gemm<2, false, 384>(acc, T2, a.w_tr[2], 384, w, FT_WAVES, lane);
+    ft_store<2, false, true>(acc, A0, 384, a.b_tr[2], w, FT_WAVES, lane);  // act += ...
     __syncthreads();
   }
-  ft_layernorm384(A0, 2 * w, a.tr_ln_s, a.tr_ln_o, lane);
-  ft_layernorm384(A0, 2 * w + 1, a.tr_ln_s, a.tr_ln_o, lane);
+  for (int nd = w; nd < FT_NODES; nd += FT_WAVES) ft_layernorm384(A0, nd, a.tr_ln_s, a.tr_ln_o, lane);
   __syncthreads();
-  for (int e = threadIdx.x; e < FT_NODES * 384; e += 512) {  // act out (the next iteration's input)
+  for (int e = threadIdx.x; e < FT_NODES * 384; e += 64 * FT_WAVES) {  // act out (the next iteration's input)
     const int n = e / 384, c = e - 384 * (e / 384);
     if (node0 + n < a.N) a.act[(node0 + n) * 384 + c] = A0[ft_at(384, n, c)];
   }
   {
     f32x4t acc[1], acc2[1];
-    if (w == 0) {  // backbone affine update (6 outputs)
+    if (w == 8) {  // backbone affine update (6 outputs)
       ft_gemm<1, false, 384>(acc, A0, a.w_aff, 6, 0, 1, lane);
       ft_store6(acc[0], a.upd, a.b_aff, node0, a.N, lane);
     }
     // sidechain input: sc_in(relu(act)) + sc_in1(relu(init_act)), wave w owns block w of 8
+    if (w < 8) {
     ft_gemm<1, true, 384>(acc, A0, a.w_sc, 128, w, 1, lane);
     ft_gemm<1, false, 128>(acc2, IR, a.w_sc1, 128, w, 1, lane);
-    {
       const int node = lane & 15;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1467,13 +1469,17 @@ __global__ __launch_bounds__(512) void k_fold_tail(FoldTailArgs a) {
       }
     }
     __syncthreads();
-    // two residual blocks: sc += rb2(relu(rb1(relu(sc))))
+    // two residual blocks: sc += rb2(relu(rb1(relu(sc)))), waves 0-7 one block each
     for (int rb = 0; rb < 2; ++rb) {
-      ft_gemm<1, true, 128>(acc, S0, a.w_rb[2 * rb], 128, w, 1, lane);
-      ft_store<1, true, false>(acc, S1, 128, a.b_rb[2 * rb], w, 1, lane);
+      if (w < 8) {
+        ft_gemm<1, true, 128>(acc, S0, a.w_rb[2 * rb], 128, w, 1, lane);
+        ft_store<1, true, false>(acc, S1, 128, a.b_rb[2 * rb], w, 1, lane);
+      }
       __syncthreads();
-      ft_gemm<1, false, 128>(acc, S1, a.w_rb[2 * rb + 1], 128, w, 1, lane);
-      ft_store<1, false, true>(acc, S0, 128, a.b_rb[2 * rb + 1], w, 1, lane);
+      if (w < 8) {
+        ft_gemm<1, false, 128>(acc, S1, a.w_rb[2 * rb + 1], 128, w, 1, lane);
+        ft_store<1, false, true>(acc, S0, 128, a.b_rb[2 * rb + 1], w, 1, lane);
+      }
       __syncthreads();
     }
     if (w == 0) {  // torsion angles (unnormalised, 6 outputs)
@@ -1501,15 +1507,22 @@ inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, i
     // per MFMA are the same for any split, while more slices mean more waves in flight and
     // shorter dependent chains (measured on 8 x 256 decodes: four accumulators per wave with 4/16
     // slices 7.05 ms, one with 4/8 slices 6.08 ms)
-    auto go = [&](auto kern, int slices) {
+    auto go = [&](auto kern, int slices, int nacc = 1) {
       // slice width rounded UP (to whole 4-k fragment groups): ks · slices >= K, so no tail of K is
       // dropped; the last slices may be short or empty (k1 = min(K, k0 + ks) in the kernel)
       const int ks = ((K + slices - 1) / slices + 3) / 4 * 4;
-      const dim3 grid((unsigned)(((N + 31) / 32) * ((M + 31) / 32)));  // 1-D, XCD-aware in the kernel
+      const dim3 grid((unsigned)(((N + 32 * nacc - 1) / (32 * nacc)) * ((M + 31) / 32)));  // 1-D, XCD-aware in the kernel
       hipLaunchKernelGGL(kern, grid, dim3(64 * slices), 0, st, X, ldx, Wt, N, b, Y, ldy, M, N, K, flags, ks);
     };
-    if (K >= 1024)
-      go(k_gemm_mfma<16, 1>, 16);
+    if (K >= 1024) {  // the IPA output projection (K = 2112): NACC column tiles per wave re-read X less
+      static const int nacc = getenv("PST_DECODE_WIDE_NACC") ? atoi(getenv("PST_DECODE_WIDE_NACC")) : 1;
+      if (nacc == 4 && N % 128 == 0)
+        go(k_gemm_mfma<16, 4>, 16, 4);
+      else if (nacc == 2 && N % 64 == 0)
+        go(k_gemm_mfma<16, 2>, 16, 2);
+      else
+        go(k_gemm_mfma<16, 1>, 16);
+    }
     else if (K >= 256)
       go(k_gemm_mfma<8, 1>, 8);
     else
@@ -1768,7 +1781,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
                         W.affine_update.w, W.affine_update.b, W.sc_in.w, W.sc_in.b, W.sc_in1.w, W.sc_in1.b,
                         {W.rb1.w, W.rb2.w, W.rb1_1.w, W.rb2_1.w}, {W.rb1.b, W.rb2.b, W.rb1_1.b, W.rb2_1.b},
                         W.angles.w, W.angles.b};
-        hipLaunchKernelGGL(k_fold_tail, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, ft);
+        hipLaunchKernelGGL(k_fold_tail, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(64 * FT_WAVES), 0, st, ft);
       } else {
       layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
       gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
@@ -2042,6 +2055,7 @@ int pst_decoder_destroy(pst_decoder* dec) {
   for (auto& kv : dec->graphs) (void)hipGraphExecDestroy(kv.second);
   dec->graphs.clear();
   if (dec->h_up) (void)hipHostFree(dec->h_up);
+  if (dec->h_atoms) (void)hipHostFree(dec->h_atoms);
   if (dec->up_ev) (void)hipEventDestroy(dec->up_ev);
   if (dec->stream) (void)hipStreamDestroy(dec->stream);
   delete dec;
@@ -2122,13 +2136,23 @@ int pst_decoder_decode_ex(pst_decoder* dec, const uint32_t* tokens, const int64_
     if (G.B == 0) continue;
     rc = decode_group(dec, S, G, keep);
     if (rc) return rc;
-    DCHK(hipMemcpyAsync(atom37_out + out0 * 111, S.atom37, sizeof(float) * G.N * 111, hipMemcpyDeviceToHost,
-                        dec->stream));
+    // atom37 D2H into a pinned staging buffer, then one host copy (a pageable-destination D2H is
+    // staged by the runtime in small pieces)
+    const size_t na = (size_t)G.N * 111;
+    if (na > dec->h_atoms_floats) {
+      if (dec->h_atoms) DCHK(hipHostFree(dec->h_atoms));
+      dec->h_atoms = nullptr;
+      dec->h_atoms_floats = 0;
+      DCHK(hipHostMalloc((void**)&dec->h_atoms, sizeof(float) * na));
+      dec->h_atoms_floats = na;
+    }
+    DCHK(hipMemcpyAsync(dec->h_atoms, S.atom37, sizeof(float) * na, hipMemcpyDeviceToHost, dec->stream));
     if (up_proj_out)  // quantize_post_proj: the up_proj half of each token's [PE | up_proj] row
       DCHK(hipMemcpy2DAsync(up_proj_out + token_offsets[b0] * 128, 128 * sizeof(float), S.orig_in + 128,
                             256 * sizeof(float), 128 * sizeof(float), (size_t)G.T, hipMemcpyDeviceToHost,
                             dec->stream));
     DCHK(hipStreamSynchronize(dec->stream));
+    std::memcpy(atom37_out + out0 * 111, dec->h_atoms, sizeof(float) * na);
   }
   return PST_OK;
 }
