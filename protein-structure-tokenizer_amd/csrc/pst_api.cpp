@@ -38,6 +38,11 @@ constexpr double FUSED_HALF_ROUND = 1.02;
 // Fused layers of more than one round run as a persistent queue of half tasks (k_mpnn_q): the
 // unit is 25 edge blocks, so a layer's last units are half as long and its tail half as deep.
 constexpr bool MPNN_QUEUE_DEFAULT = true;
+// Layers that run as the queue (bit l = layer l) when the queue is on: layer 0 (no edge MLP, its
+// edge inputs from the PE tables) runs faster as k_mpnn<0, false> at every size measured —
+// 1 024 / 512 / 256 proteins 8.24-8.30 / 4.15-4.21 / 2.08-2.09 ms against 8.42 / 4.34-4.37 /
+// 2.12 ms as the queue (profiles/r04_ab_qgroup.txt) — layers 1 and 2 gain from it.
+constexpr int64_t MPNN_QUEUE_LAYERS = 6;
 bool use_half_tasks(int64_t n_tasks, int64_t n_simds) { return 2 * n_tasks > n_simds && n_tasks <= n_simds; }
 bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
   const int64_t k = (n_tasks + n_simds - 1) / n_simds;
@@ -252,6 +257,8 @@ struct pst_ctx {
   int64_t half_tasks = -2;   // PST_HALF_TASKS: 1 = fused layers always two waves per task, 0 = never; -1 = policy
   int64_t mpnn_qwaves = -2;  // PST_MPNN_QWAVES: 4 = two 4-wave queue workgroups per CU; else one 8-wave workgroup
                              // per CU with all of W1 in LDS (k_mpnn<0..2> -1.0..-2.8 %, profiles/r04_ab_qwaves.txt)
+  int64_t mpnn_qgroup = -2;  // PST_MPNN_QGROUP: queue unit order, tasks per group (0 = halves adjacent); -1 = wave slots per XCD
+  int64_t mpnn_queue_layers = -2;  // PST_MPNN_QUEUE_LAYERS: layer mask of the queue form; -1 = MPNN_QUEUE_LAYERS
   int64_t mpnn_queue = -2;   // PST_MPNN_QUEUE: 1 = fused layers as the half-task queue (k_mpnn_q) whenever not
                              // k_mpnn<L, true>, 0 = never (k_mpnn<L, false>); -1 = policy
   std::vector<int64_t> h_offsets;
@@ -643,6 +650,8 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   env_threshold(ctx->mpnn_queue, "PST_MPNN_QUEUE");
   const bool queue = !split && !half && (ctx->mpnn_queue >= 0 ? ctx->mpnn_queue != 0 : MPNN_QUEUE_DEFAULT);
   ctx->last_sched = split ? 2 : half ? 1 : queue ? 3 : 0;
+  env_threshold(ctx->mpnn_queue_layers, "PST_MPNN_QUEUE_LAYERS");
+  const int64_t queue_layers = ctx->mpnn_queue_layers >= 0 ? ctx->mpnn_queue_layers : MPNN_QUEUE_LAYERS;
   if (queue) HIPCHK(hipMemsetAsync(w.qctr, 0, sizeof(int32_t) * 3 * (128 + n_tasks), st));
   float* msg_rows = nullptr;
   int32_t bpw = 1;
@@ -674,12 +683,15 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.blocks_per_wave = bpw;
     m.half_tasks = half ? 1 : 0;
     m.clk = ctx->d_clk + 8 * l;
-    if (queue) {
+    if (queue && ((queue_layers >> l) & 1)) {
       m.q_head = w.qctr + l * (128 + n_tasks);
       m.q_done = m.q_head + 128;
       m.q_grid = 2 * (ctx->n_simds / 4);  // two 4-wave workgroups per CU (MPNN_MIN_BLOCKS)
       env_threshold(ctx->mpnn_qwaves, "PST_MPNN_QWAVES");
       m.q_waves = ctx->mpnn_qwaves == 4 ? 4 : 8;
+      env_threshold(ctx->mpnn_qgroup, "PST_MPNN_QGROUP");
+      // wave slots of one XCD: q_grid x 4 waves over 8 XCDs (both workgroup sizes hold that many)
+      m.q_group = (int32_t)(ctx->mpnn_qgroup >= 0 ? ctx->mpnn_qgroup : m.q_grid * 4 / 8);
     }
     m.senders = w.senders;
     m.deg = w.deg;

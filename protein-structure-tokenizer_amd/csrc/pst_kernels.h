@@ -92,6 +92,9 @@ struct MpnnArgs {
   int32_t* q_done;
   int64_t q_grid;
   int32_t q_waves;  // 4 or 8 waves per queue workgroup (k_mpnn_q<L, NW>)
+  // unit order within an XCD's queue: groups of q_group tasks, first halves of the group before
+  // its second halves (0 = halves of a task adjacent: units 2t, 2t+1)
+  int32_t q_group;
   // clock / occupancy stamps (measurement, 8 u64, see ClockStamp and pst_clock_counters); null = off
   unsigned long long* clk;
   // outputs

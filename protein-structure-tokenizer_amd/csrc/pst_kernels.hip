@@ -979,8 +979,12 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
 // wave that completes the SECOND half of a task (told by the value its add on the task's counter
 // returns) runs the task's node update alone, as k_mpnn<L, false> does. Same operations in the
 // same order as the other fused forms: identical bits.
-// Queues: one per XCD (tasks split into 8 contiguous ranges, units 2t, 2t+1 = the halves of task
-// t), a wave pulls from its own XCD's queue (s_getreg XCC_ID; locality only) and, once that is
+// Queues: one per XCD (tasks split into 8 contiguous ranges of units). Unit order: groups of
+// q_group tasks (the wave slots of one XCD), the group's first halves, then its second halves —
+// so a launch of exactly one wave per task-slot runs like k_mpnn<L, false> (each wave: two halves,
+// then the node update), where adjacent halves (q_group 0: units 2t, 2t+1 = the halves of task
+// t) ran both halves at once and left the node updates of one half of the waves in series with
+// the next units of the other half. A wave pulls from its own XCD's queue (s_getreg XCC_ID; locality only) and, once that is
 // empty, from the next ones in turn; it leaves after finding all eight empty (every exit path is
 // bounded: one failed pull per queue). The halves of a task may run on different XCDs, so the
 // segment-sum hand-off is the agent-scope release / acquire pair (MI355X_MICROARCH.md,
@@ -1025,9 +1029,23 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_mpnn_q(MpnnArgs a_in) {
       q = (q + 1) & 7;
       continue;
     }
-    const int64_t task = t0 + (j >> 1);
-    const int hh = j & 1;
-    mpnn_edge_blocks<LAYER, KL, NW>(a, task, lane, 25 * hh, 25 * hh + 25, w1_lds, lds_scratch, w);
+    int64_t task;
+    int hh;
+    const int G = a.q_group;
+    if (G > 0) {  // group g: tasks gG .. gG+gs-1, their first halves, then their second halves
+      const int g = j / (2 * G), r = j - 2 * G * g;
+      const int64_t rest = t1 - t0 - (int64_t)g * G;
+      const int gs = rest < G ? (int)rest : G;
+      hh = r >= gs;
+      task = t0 + (int64_t)g * G + (r - hh * gs);
+    } else {
+      task = t0 + (j >> 1);
+      hh = j & 1;
+    }
+    // the lane index re-made opaque per unit: nothing lane-derived is hoisted out of the loop
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    mpnn_edge_blocks<LAYER, KL, NW>(a, task, ln, 25 * hh, 25 * hh + 25, w1_lds, lds_scratch, w);
     // hand-off of this half's segment sums: stores drained, agent release, then the counter
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1038,7 +1056,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_mpnn_q(MpnnArgs a_in) {
     if (prev == 1) {  // both halves done: this wave runs the node update
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      mpnn_node_tile<LAYER>(a, task * 32, lane, a.agg + task * 32 * 128);
+      mpnn_node_tile<LAYER>(a, task * 32, ln, a.agg + task * 32 * 128);
     }
   }
   cs.stop(a_k->clk);
