@@ -286,6 +286,22 @@ def clock_stats(per_step):
             "stamped_ms": round(float(c[..., 1].sum() / 1e5), 1)}
 
 
+def wave_slot_occupancy(per_step, slots):
+    """Wave-slot occupancy of each MPNN layer launch (one launch per layer per step): the sum of
+    its waves' lifetimes over slots x (last end - first start), from the same clock counters
+    (clk[2] lifetimes, clk[3] min start, clk[4] max end, 100 MHz ticks). 1 - occupancy is the
+    launch's idle slot time: ramp, tail and any slot a wave leaves empty."""
+    if not per_step:
+        return None
+    c = np.array(per_step, np.float64)  # [steps, 3, 8]
+    span = c[:, :, 4] - c[:, :, 3]
+    if (span <= 0).any():
+        return None
+    occ = (c[:, :, 2] / (slots * span)).mean(0)
+    return {"per_layer": [round(float(x), 4) for x in occ], "slots": int(slots),
+            "waves_per_launch": [int(x) for x in c[0, :, 5]]}
+
+
 def casp14_end_to_end(tk):
     """SURVEY config 2 as the CLI runs it: parse the 31 CASP14 PDB files (native parser), tokenize
     from host buffers, write <stem>_tokens.npy. Reported beside `value`."""
@@ -558,16 +574,24 @@ def main():
         stage = st if stage is None else {k: stage[k] + st[k] for k in st}
         sclk.append(tk.clock_counters(reset=True))
     stage_clock = clock_stats(sclk)
+    # two waves per SIMD (the MPNN kernels' 256 VGPRs), four SIMDs per CU
+    occupancy = wave_slot_occupancy(sclk, 8 * torch.cuda.get_device_properties(dev).multi_processor_count)
     stage = {k: v / 3 for k, v in stage.items()}
     tk.set_timing(False)
 
     kern = {}
-    for name in ("mpnn0", "mpnn1", "mpnn2"):
-        ex = MFMA_PER_TASK[name] * MFMA_FLOP * (R / 32) / (stage[name] * 1e-3) / 1e12
-        kern[name] = {"launch_ms": round(stage[name], 3), "executed_mfma_tflops": round(ex, 2),
+    # layers 1-2 as one launch (k_mpnn_x, PST_MPNN_XLAYER): its time lands in stage mpnn2
+    xlayer = stage["mpnn1"] < 0.05 * stage["mpnn2"]
+    groups = (("mpnn0", ("mpnn0",)), ("mpnn12", ("mpnn1", "mpnn2"))) if xlayer else \
+        tuple((n, (n,)) for n in ("mpnn0", "mpnn1", "mpnn2"))
+    for name, parts in groups:
+        ms = sum(stage[p] for p in parts)
+        ex = sum(MFMA_PER_TASK[p] for p in parts) * MFMA_FLOP * (R / 32) / (ms * 1e-3) / 1e12
+        kern[name] = {"launch_ms": round(ms, 3), "executed_mfma_tflops": round(ex, 2),
                       "frac": round(ex / PEAK_FP32_TFLOPS, 4)}
-    dom_ms = stage["mpnn1"]
-    executed = kern["mpnn1"]["executed_mfma_tflops"]
+    dom = "mpnn12" if xlayer else "mpnn1"
+    dom_ms = kern[dom]["launch_ms"]
+    executed = kern[dom]["executed_mfma_tflops"]
     traffic = None
     if os.path.exists(args.traffic_file):
         with open(args.traffic_file) as fh:
@@ -578,7 +602,8 @@ def main():
                    "achieved_GBps": round(per_res * R / (dom_ms * 1e-3) / 1e9, 1),
                    "source": tf.get("source", args.traffic_file)}
     roofline = {
-        "kernel": "k_mpnn<1> (edge MLP L1 + message MLP L2 + node FFN, fused)",
+        "kernel": ("k_mpnn_x (layers 1-2 as one persistent queue)" if xlayer else
+                   "k_mpnn<1> (edge MLP L1 + message MLP L2 + node FFN, fused)"),
         "bound": "mfma", "achieved": executed, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": round(executed / PEAK_FP32_TFLOPS, 4),
         "traffic": traffic["bytes_per_launch"] if traffic else None,  # HBM bytes per launch (PMC)
@@ -587,13 +612,14 @@ def main():
                 "SQ_INSTS_MFMA) / HIP-event launch time; effective_alg_tflops counts SURVEY 8d's algorithmic "
                 "FLOPs instead, which the kernel's algebraic rewrites (DESIGN.md 5) execute in 0.52x the work",
         "launch_ms": round(dom_ms, 3),
-        "effective_alg_tflops": round(MPNN1_ALG_FLOP_PER_RES * R / (dom_ms * 1e-3) / 1e12, 2),
+        "effective_alg_tflops": round(MPNN1_ALG_FLOP_PER_RES * (2 if xlayer else 1) * R / (dom_ms * 1e-3) / 1e12, 2),
         # the peak is quoted at the 2.4 GHz spec clock; at the clock the chip actually held under
         # k_mpnn<1> in the stage-timing steps (its launches' clock stamps) the reachable peak is
         # peak x clock / 2.4
         "stage_clock": stage_clock,
         "frac_at_measured_clock": (round(executed / (PEAK_FP32_TFLOPS * stage_clock["per_layer_ghz"][1] / SPEC_GHZ), 4)
                                    if stage_clock else None),
+        "wave_slot_occupancy": occupancy,
         "kernels": kern,
         "stage_ms": {k: round(v, 3) for k, v in stage.items()},
         "path_effective_alg_tflops": (round(PATH_ALG_FLOP_PER_RES[args.df] * R / (sum(stage.values()) * 1e-3) / 1e12, 2)

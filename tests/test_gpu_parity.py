@@ -366,15 +366,19 @@ def test_mpnn_queue_identical_at_full_rounds(monkeypatch):
     # queue on every layer with the default unit order (groups of one XCD's wave slots), with
     # adjacent halves (group 0), and the default layers with a group size that leaves a partial
     # group in every XCD's range (3 072 / 8 = 384 tasks = 10 x 37 + 14)
-    for queue, layers, group in (("0", "-", "-"), ("1", "7", "-"), ("1", "7", "0"), ("1", "-", "37")):
+    # and layers 1-2 as one persistent launch (k_mpnn_x: cross-layer waits), 4- and 8-wave groups
+    for queue, layers, group, xl, qw in (("0", "-", "-", "0", "-"), ("1", "7", "-", "0", "-"),
+                                         ("1", "7", "0", "0", "-"), ("1", "-", "37", "0", "-"),
+                                         ("1", "-", "-", "1", "-"), ("1", "-", "-", "1", "4")):
         monkeypatch.setenv("PST_MPNN_QUEUE", queue)
-        for k, v in (("PST_MPNN_QUEUE_LAYERS", layers), ("PST_MPNN_QGROUP", group)):
+        for k, v in (("PST_MPNN_QUEUE_LAYERS", layers), ("PST_MPNN_QGROUP", group), ("PST_MPNN_XLAYER", xl),
+                     ("PST_MPNN_QWAVES", qw)):
             if v == "-":
                 monkeypatch.delenv(k, raising=False)
             else:
                 monkeypatch.setenv(k, v)
         tk = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
-        for rep in range(3 if layers == "7" and group == "-" else 1 if queue == "0" else 2):
+        for rep in range(3 if (layers == "7" and group == "-") or xl == "1" else 1 if queue == "0" else 2):
             tok, nt, nn = tk.tokenize_packed(pos.astype(np.float32), flags, off)
             assert tk.last_plan_detail()["schedules"] == (["fused_queue"] if queue == "1" else ["fused"])
             hl = [tk.debug_fetch(w, R) for w in (1, 2, 3)]
