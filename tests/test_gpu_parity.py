@@ -390,3 +390,38 @@ def test_mpnn_queue_identical_at_full_rounds(monkeypatch):
         for a, b in zip(o[1], base[1]):
             assert np.array_equal(a, b)
         assert np.array_equal(o[2], base[2])
+
+
+@pytest.mark.parametrize("lens", [(50,), (50, 51), (130, 77, 301, 52, 64)])
+def test_mpnn_queue_forced_on_small_batches(lens, monkeypatch):
+    """The persistent queue forced onto batches far below one round (4 to 20 tasks: most XCD
+    ranges empty, a wave finds its own queue empty and steals from the others; the unit group larger
+    than a range) on every layer, with the default unit order and with adjacent halves, and the
+    cross-layer launch: node features after every layer and tokens equal the default schedule's
+    bit for bit."""
+    from pst_amd._native import Tokenizer, pack_samples
+    samples = [synthetic.synthetic_protein(n, 5100 + i) for i, n in enumerate(lens)]
+    pos, flags, off = pack_samples(samples)
+    R = int(off[-1])
+    monkeypatch.setenv("PST_DEBUG", "1")
+    ref = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
+    tok0, _, _ = ref.tokenize_packed(pos, flags, off)
+    h0 = [ref.debug_fetch(w, R).view(np.uint32).copy() for w in (1, 2, 3)]
+    ref.close()
+    for env in ({"PST_MPNN_QUEUE_LAYERS": "7"}, {"PST_MPNN_QUEUE_LAYERS": "7", "PST_MPNN_QGROUP": "0"},
+                {"PST_MPNN_XLAYER": "1"}):
+        monkeypatch.setenv("PST_SPLIT_TASKS", "0")
+        monkeypatch.setenv("PST_HALF_TASKS", "0")
+        monkeypatch.setenv("PST_MPNN_QUEUE", "1")
+        for k in ("PST_MPNN_QUEUE_LAYERS", "PST_MPNN_QGROUP", "PST_MPNN_XLAYER"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        tk = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
+        tok, _, _ = tk.tokenize_packed(pos, flags, off)
+        assert tk.last_plan_detail()["schedules"] == ["fused_queue"]
+        for w, b in zip((1, 2, 3), h0):
+            assert np.array_equal(tk.debug_fetch(w, R).view(np.uint32), b), (env, w)
+        assert np.array_equal(tok[:R], tok0[:R]), env
+        tk.close()
+
