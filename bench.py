@@ -200,7 +200,8 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
     """Token ids of the fixture proteins this rank holds vs the reference's own forward
     (Vq3D.encode_and_quantize under the shim, float64 with JAX's float32 PE argument, i.e. the
     reference's PE values): the headline workload's exact-match sample, every 8th protein
-    (forward_ref_bench.npz, 128 proteins, make_forward_bench.py), plus the proteins of
+    (forward_ref_bench.npz, 128 proteins, make_forward_bench.py; config 5's workload: every 16th,
+    32 proteins), plus the proteins of
     forward_ref_wide.npz the workload holds (bench256 p0-7, 200, 511, 777, 1023; bench512 p0-1 at
     64000/df 4). With `bounded` (our FSQ-bounded latents, pst_aux) the report carries our
     deviation from the reference's latent and its ratio to the rounding margin (refwide.report)."""
@@ -209,8 +210,11 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
         F = refwide.load()
     except Exception:
         return None
+    # the bench fixture's sample of this workload: config 3 (bench256_*, every 8th protein) or
+    # config 5 (bench512_*, every 16th)
+    bkey = {(4096, 1, 256): "bench256_p{}", (64000, 4, 512): "bench512_p{}"}.get((args.codebook, args.df, args.residues))
     try:
-        FB = refwide.load_bench() if (args.codebook, args.df, args.residues) == (4096, 1, 256) else None
+        FB = refwide.load_bench() if bkey else None
     except Exception:
         FB = None
     tag = {(4096, 1, 256): "bench256_p{}_k4096_df1", (64000, 4, 512): "bench512_p{}_k64000_df4"}.get(
@@ -219,8 +223,8 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
         return None
     reps, prots, src = [], [], {}
     for i, p in enumerate(ids):
-        if FB is not None and f"bench256_p{p}/tokens_pe32" in FB.files:
-            c, G, want = f"bench256_p{p}", FB, None
+        if FB is not None and bkey.format(p) + "/tokens_pe32" in FB.files:
+            c, G, want = bkey.format(p), FB, None
         elif tag.format(p) + "/tokens" in F.files:
             c, G = tag.format(p), F
             want = F[c + "/tokens"]
@@ -388,8 +392,10 @@ def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=No
         out[threads], toks = _ref_as_computed_rate(model, pf, args.df, threads, cores,
                                                    f"every {max(1, nb // max(1, n))}th protein of the workload")
         if ident is None:
-            ident = sum(int(np.sum(t[:off[i + 1] - off[i]] == gpu_tok[off[i]:off[i + 1]])) for t, i in zip(toks, csel))
-            out[threads]["tokens_identical_to_gpu"] = f"{ident} / {int(sum(off[i + 1] - off[i] for i in csel))}"
+            # protein i's T = n_i / df tokens sit at gpu_tok[off[i] .. off[i] + T) (raw-offset layout)
+            ms = [min(len(t), int(off[i + 1] - off[i]) // args.df) for t, i in zip(toks, csel)]
+            ident = sum(int(np.sum(t[:m] == gpu_tok[off[i]:off[i] + m])) for t, i, m in zip(toks, csel, ms))
+            out[threads]["tokens_identical_to_gpu"] = f"{ident} / {sum(ms)}"
     cfg2 = {}
     if casp is not None and args.codebook == 4096 and args.df == 1:
         cpos, cflags, coff, ctok = casp

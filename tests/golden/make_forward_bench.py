@@ -7,13 +7,17 @@ them — the `_pe32` rendering of `make_forward_wide.py` (float64 with the sinus
 rounded to float32 exactly as JAX forms it with x64 off, i.e. the reference's own PE values) —
 at codebook 4096, df 1, random weights `params.random_params(6, 1234)` (the bench's).
 
+`--config 5` does the same for SURVEY config 5's workload (`bench.py --codebook 64000 --df 4
+--residues 512 --proteins 512`: synthetic_batch(512, 512, seed=1000)), every 16th protein (32
+proteins, 4 096 tokens), case names `bench512_p{p}`, in the same file.
+
 Kept per protein `bench256_p{p}`: the reference's token ids, its FSQ-bounded latents (float64),
 the per-token rounding margin, `meta` = [n, T, codebook, df, D, seed], and the SHA-256 of the
 float32 inputs plus the generator arguments. The inputs themselves are NOT stored: they are
 regenerated from `pst_amd.synthetic.synthetic_protein(256, 1000 + p)` and must hash to the stored
 SHA (`tests/test_fixture_recipes.py`), which keeps the file small and the recipe honest.
 
-    python tests/golden/make_forward_bench.py [--jobs 7] [--stride 8]
+    python tests/golden/make_forward_bench.py [--jobs 7] [--stride 8] [--config 3|5]
 """
 import argparse
 import os
@@ -25,7 +29,14 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "forward_ref_bench.npz")
-N_PROT, N_RES, SEED0, CODEBOOK, DF = 1024, 256, 1000, 4096, 1
+# SURVEY config -> (proteins, residues, seed of protein 0, codebook, df, default stride)
+CONFIGS = {3: (1024, 256, 1000, 4096, 1, 8), 5: (512, 512, 1000, 64000, 4, 16)}
+N_PROT, N_RES, SEED0, CODEBOOK, DF, _ = CONFIGS[3]
+
+
+def set_config(cfg):
+    global N_PROT, N_RES, SEED0, CODEBOOK, DF
+    N_PROT, N_RES, SEED0, CODEBOOK, DF, _ = CONFIGS[cfg]
 
 
 def proteins(stride=8):
@@ -33,10 +44,12 @@ def proteins(stride=8):
 
 
 def case_name(p):
-    return f"bench256_p{p}"
+    return f"bench{N_RES}_p{p}"
 
 
-def run_one(p):
+def run_one(job):
+    cfg, p = job
+    set_config(cfg)
     sys.path.insert(0, HERE)
     import make_forward_wide as M
     t0 = time.time()
@@ -57,19 +70,22 @@ def run_one(p):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=7)
-    ap.add_argument("--stride", type=int, default=8)
+    ap.add_argument("--stride", type=int, default=None)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     args = ap.parse_args()
+    set_config(args.config)
+    stride = args.stride or CONFIGS[args.config][5]
     sys.path.insert(0, HERE)
     import _refenv
     if not _refenv.available():
         sys.exit("reference not available")
     sys.path.insert(0, _refenv.PKG)
     old = dict(np.load(OUT)) if os.path.exists(OUT) else {}
-    todo = [p for p in proteins(args.stride) if f"{case_name(p)}/tokens_pe32" not in old]
+    todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old]
     print(f"{len(todo)} proteins to run", flush=True)
     done = 0
     with get_context("spawn").Pool(args.jobs) as pool:
-        for p, res, dt in pool.imap_unordered(run_one, todo):
+        for p, res, dt in pool.imap_unordered(run_one, [(args.config, p) for p in todo]):
             for k, v in res.items():
                 old[f"{case_name(p)}/{k}"] = v
             done += 1

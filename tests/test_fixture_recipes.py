@@ -42,13 +42,15 @@ def test_casp14_inputs_match_atom37_fixture():
 
 
 def test_bench_fixture_inputs_reproduce():
-    """forward_ref_bench.npz stores no inputs: every 8th protein of bench.py's workload must
-    regenerate to the SHA-256 the reference forward ran on."""
+    """forward_ref_bench.npz stores no inputs: every 8th protein of bench.py's workload (and every
+    16th of config 5's) must regenerate to the SHA-256 the reference forward ran on."""
     FB = refwide.load_bench()
+    assert refwide.cases(FB, "bench256_") == sorted(f"bench256_p{p}" for p in range(0, 1024, 8))
+    # config 5's sample (make_forward_bench.py --config 5): every 16th of 512 x 512 residues
+    assert refwide.cases(FB, "bench512_") == sorted(f"bench512_p{p}" for p in range(0, 512, 16))
     names = refwide.cases(FB)
-    assert names == sorted(f"bench256_p{p}" for p in range(0, 1024, 8))
     for c in names:
         n_res, seed = (int(v) for v in FB[c + "/synthetic_args"])
-        assert (n_res, seed) == (256, 1000 + int(c.split("_p")[1]))
+        assert (n_res, seed) == (int(c[5:8]), 1000 + int(c.split("_p")[1]))
         s = synthetic.synthetic_protein(n_res, seed)
         assert M.input_sha(s.atom37_positions.astype(np.float32), s.atom_flags()) == str(FB[c + "/input_sha256"]), c

@@ -69,7 +69,7 @@ def test_gpu_tokens_equal_reference_bench_sample():
     from pst_amd import synthetic
     from pst_amd._native import pack_samples
     FB = refwide.load_bench()
-    names = refwide.cases(FB)
+    names = refwide.cases(FB, "bench256_")
     samples = [synthetic.synthetic_protein(*(int(v) for v in FB[c + "/synthetic_args"])) for c in names]
     pos, flags, off = pack_samples(samples)
     tk = _make(4096, 1, 6, 1234)
@@ -86,3 +86,31 @@ def test_gpu_tokens_equal_reference_bench_sample():
     r = refwide.merge(reps)
     print({k: r[k] for k in ("tokens", "identical", "min_margin", "max_deviation", "max_deviation_over_margin")})
     assert r["tokens"] == 32768 and r["identical"] == r["tokens"], r
+
+
+def test_gpu_tokens_equal_reference_config5_sample():
+    """SURVEY config 5's exact-match sample: every 16th protein of bench.py's 512 x 512-residue
+    codebook-64 000 / df-4 workload (forward_ref_bench.npz bench512_*, 32 proteins, 4 096 tokens) in
+    one ragged batch through the C ABI, against the reference's forward (_pe32 rendering)."""
+    from pst_amd import synthetic
+    from pst_amd._native import pack_samples
+    FB = refwide.load_bench()
+    names = refwide.cases(FB, "bench512_")
+    assert len(names) == 32
+    samples = [synthetic.synthetic_protein(*(int(v) for v in FB[c + "/synthetic_args"])) for c in names]
+    pos, flags, off = pack_samples(samples)
+    tk = _make(64000, 4, 6, 1234)
+    tok, nt, nn = tk.tokenize_packed(pos.astype(np.float32), flags, off)
+    b = tk.aux(int(off[-1]))["bounded"]
+    tk.close()
+    reps = []
+    for i, c in enumerate(names):
+        n, T = (int(v) for v in FB[c + "/meta"][:2])
+        assert nn[i] == n and nt[i] == T
+        a = int(off[i])
+        assert np.abs(b[a:a + T] - FB[c + "/bounded_pe32"]).max() < TOL["_pe32"][1], c
+        reps.append(refwide.report(FB[c + "/bounded_pe32"], FB[c + "/tokens_pe32"], b[a:a + T], tok[a:a + T]))
+    r = refwide.merge(reps)
+    print({k: r[k] for k in ("tokens", "identical", "min_margin", "max_deviation", "max_deviation_over_margin")})
+    assert r["tokens"] == 4096 and r["identical"] == r["tokens"], r
+

@@ -121,7 +121,7 @@ def _bench_inputs(c):
 
 
 def test_oracle_tokens_equal_reference_bench_sample():
-    names = refwide.cases(FB)
+    names = refwide.cases(FB, "bench256_")
     assert len(names) == 128
 
     def run(c):
@@ -143,3 +143,31 @@ def test_oracle_tokens_equal_reference_bench_sample():
     print({k: r[k] for k in ("tokens", "identical", "min_margin", "max_deviation", "max_deviation_over_margin")})
     assert r["tokens"] == 32768
     assert r["identical"] == r["tokens"], r
+
+
+def test_oracle_tokens_equal_reference_config5_sample():
+    """SURVEY config 5 (codebook 64 000, df 4, 512-residue proteins): every 16th protein of
+    bench.py's --codebook 64000 --df 4 --residues 512 --proteins 512 workload (32 proteins, 4 096
+    tokens), the C oracle against the reference's forward."""
+    names = refwide.cases(FB, "bench512_")
+    assert len(names) == 32
+
+    def run(c):
+        pos, fl = _bench_inputs(c)
+        return c, O.tokenize(P.random_blob(6, 1234), LEVELS[64000], 4, pos, fl)
+
+    with ThreadPoolExecutor(8) as ex:
+        outs = dict(ex.map(run, names))
+    reps = []
+    for c in names:
+        n, T, cb, df, D, seed = (int(v) for v in FB[c + "/meta"])
+        assert (cb, df, D, seed) == (64000, 4, 6, 1234)
+        out = outs[c]
+        assert out["graph"]["n"] == n and len(out["tokens"]) == T
+        assert np.abs(out["b"] - FB[c + "/bounded_pe32"]).max() < TOL["_pe32"][1], c
+        reps.append(refwide.report(FB[c + "/bounded_pe32"], FB[c + "/tokens_pe32"], out["b"], out["tokens"]))
+    r = refwide.merge(reps)
+    print({k: r[k] for k in ("tokens", "identical", "min_margin", "max_deviation", "max_deviation_over_margin")})
+    assert r["tokens"] == 4096
+    assert r["identical"] == r["tokens"], r
+
