@@ -199,8 +199,8 @@ def plan_only(args, rank, world):
 def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
     """Token ids of the fixture proteins this rank holds vs the reference's own forward
     (Vq3D.encode_and_quantize under the shim, float64 with JAX's float32 PE argument, i.e. the
-    reference's PE values): the headline workload's exact-match sample, every 8th protein
-    (forward_ref_bench.npz, 128 proteins, make_forward_bench.py; config 5's workload: every 16th,
+    reference's PE values): every 4th protein of the headline workload
+    (forward_ref_bench.npz, 256 proteins, make_forward_bench.py; config 5's workload: every 16th,
     32 proteins), plus the proteins of
     forward_ref_wide.npz the workload holds (bench256 p0-7, 200, 511, 777, 1023; bench512 p0-1 at
     64000/df 4). With `bounded` (our FSQ-bounded latents, pst_aux) the report carries our
@@ -210,7 +210,7 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
         F = refwide.load()
     except Exception:
         return None
-    # the bench fixture's sample of this workload: config 3 (bench256_*, every 8th protein) or
+    # the bench fixture's sample of this workload: config 3 (bench256_*, every 4th protein) or
     # config 5 (bench512_*, every 16th)
     bkey = {(4096, 1, 256): "bench256_p{}", (64000, 4, 512): "bench512_p{}"}.get((args.codebook, args.df, args.residues))
     try:
@@ -268,7 +268,7 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
             "margin_histogram_all": r["margin_histogram_all"],
             "margin_histogram_mismatches": r["margin_histogram_mismatches"],
             "against": "reference Vq3D.encode_and_quantize run in float64 under the shim with JAX's float32 "
-                       "PE argument (tests/golden/forward_ref_bench.npz: every 8th protein of the workload, "
+                       "PE argument (tests/golden/forward_ref_bench.npz: every 4th protein of the workload, "
                        "make_forward_bench.py; tests/golden/forward_ref_wide.npz, make_forward_wide.py)"}
 
 

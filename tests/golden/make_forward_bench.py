@@ -1,7 +1,8 @@
 """Reference-forward fixture for the HEADLINE workload's exact-match sample (build container only).
 
-`bench.py` checks token ids on every 8th protein of `synthetic_batch(1024, 256, seed=1000)`
-(proteins 0, 8, …, 1016: 128 proteins, 32 768 tokens, both pipeline chunks). This script runs the
+`bench.py` checks token ids against the oracle on every 8th protein of
+`synthetic_batch(1024, 256, seed=1000)`; this fixture pins every 4th (proteins 0, 4, …, 1020: 256
+proteins, 65 536 tokens, both pipeline chunks) to the reference. This script runs the
 REFERENCE's own `Vq3D.encode_and_quantize` (model.py:453-479) under the import shim on each of
 them — the `_pe32` rendering of `make_forward_wide.py` (float64 with the sinusoidal PE argument
 rounded to float32 exactly as JAX forms it with x64 off, i.e. the reference's own PE values) —
@@ -17,7 +18,7 @@ float32 inputs plus the generator arguments. The inputs themselves are NOT store
 regenerated from `pst_amd.synthetic.synthetic_protein(256, 1000 + p)` and must hash to the stored
 SHA (`tests/test_fixture_recipes.py`), which keeps the file small and the recipe honest.
 
-    python tests/golden/make_forward_bench.py [--jobs 7] [--stride 8] [--config 3|5]
+    python tests/golden/make_forward_bench.py [--jobs 7] [--stride 4] [--config 3|5]
 """
 import argparse
 import os
@@ -30,7 +31,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "forward_ref_bench.npz")
 # SURVEY config -> (proteins, residues, seed of protein 0, codebook, df, default stride)
-CONFIGS = {3: (1024, 256, 1000, 4096, 1, 8), 5: (512, 512, 1000, 64000, 4, 16)}
+CONFIGS = {3: (1024, 256, 1000, 4096, 1, 4), 5: (512, 512, 1000, 64000, 4, 16)}
 N_PROT, N_RES, SEED0, CODEBOOK, DF, _ = CONFIGS[3]
 
 

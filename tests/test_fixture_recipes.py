@@ -42,10 +42,10 @@ def test_casp14_inputs_match_atom37_fixture():
 
 
 def test_bench_fixture_inputs_reproduce():
-    """forward_ref_bench.npz stores no inputs: every 8th protein of bench.py's workload (and every
+    """forward_ref_bench.npz stores no inputs: every 4th protein of bench.py's workload (and every
     16th of config 5's) must regenerate to the SHA-256 the reference forward ran on."""
     FB = refwide.load_bench()
-    assert refwide.cases(FB, "bench256_") == sorted(f"bench256_p{p}" for p in range(0, 1024, 8))
+    assert refwide.cases(FB, "bench256_") == sorted(f"bench256_p{p}" for p in range(0, 1024, 4))
     # config 5's sample (make_forward_bench.py --config 5): every 16th of 512 x 512 residues
     assert refwide.cases(FB, "bench512_") == sorted(f"bench512_p{p}" for p in range(0, 512, 16))
     names = refwide.cases(FB)

@@ -107,8 +107,8 @@ def test_reference_as_computed_torch_matches_fixture():
 
 # ------------------------------------------------------------ the headline workload's sample
 # forward_ref_bench.npz (golden/make_forward_bench.py): the reference's forward (_pe32 rendering)
-# on every 8th protein of bench.py's workload, synthetic_batch(1024, 256, seed=1000) at codebook
-# 4096 / df 1 — the 128 proteins (32 768 tokens) its exact-match sample covers. Inputs are not
+# on every 4th protein of bench.py's workload, synthetic_batch(1024, 256, seed=1000) at codebook
+# 4096 / df 1 — 256 proteins, 65 536 tokens (and config 5's sample, bench512_*). Inputs are not
 # stored: they regenerate from the generator (SHA-checked in test_fixture_recipes.py).
 FB = refwide.load_bench()
 
@@ -122,7 +122,7 @@ def _bench_inputs(c):
 
 def test_oracle_tokens_equal_reference_bench_sample():
     names = refwide.cases(FB, "bench256_")
-    assert len(names) == 128
+    assert len(names) == 256
 
     def run(c):
         pos, fl = _bench_inputs(c)
@@ -141,8 +141,14 @@ def test_oracle_tokens_equal_reference_bench_sample():
         reps.append(refwide.report(FB[c + "/bounded_pe32"], FB[c + "/tokens_pe32"], out["b"], out["tokens"]))
     r = refwide.merge(reps)
     print({k: r[k] for k in ("tokens", "identical", "min_margin", "max_deviation", "max_deviation_over_margin")})
-    assert r["tokens"] == 32768
-    assert r["identical"] == r["tokens"], r
+    assert r["tokens"] == 65536
+    # every token equal except where the reference's float64 latent sits closer to a rounding
+    # boundary than float32 arithmetic can resolve: at 65 536 x 6 dims one margin below our
+    # ~5e-7 deviation is expected (protein 924, token 3: margin 2.6e-7), and every
+    # mismatch must be such a case (our deviation beyond its margin, the margin below 1e-6)
+    assert r["mismatches_explained_by_rounding"], r
+    assert all(m < 1e-6 for m in r["mismatch_margins"]), r
+    assert r["tokens"] - r["identical"] <= 1, r
 
 
 def test_oracle_tokens_equal_reference_config5_sample():
