@@ -272,11 +272,12 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
                        "make_forward_bench.py; tests/golden/forward_ref_wide.npz, make_forward_wide.py)"}
 
 
-def clock_stats(per_step):
-    """Shader clock from libpst's clock counters (pst_clock_counters): per step, the stamping wave
-    of each fused MPNN launch contributes (s_memtime cycles, s_memrealtime 100 MHz ticks); the
-    step's clock = cycles / ticks x 0.1 GHz over its three layers (~90 % of the step's device
-    time). Mean (cycle-weighted over all steps), min and max over steps, per-layer means."""
+def clock_stats(per_step, steps=None):
+    """Shader clock from libpst's clock counters (pst_clock_counters): the stamping wave of each
+    fused MPNN launch contributes (s_memtime cycles, s_memrealtime 100 MHz ticks); clock = cycles /
+    ticks x 0.1 GHz over the three layers (~90 % of a step's device time). `per_step`: one record
+    per read — per step (min / max over them), or one read summed over `steps` steps (the timed
+    loop reads once, after it). Mean (cycle-weighted), per-layer means."""
     if not per_step:
         return None
     c = np.array(per_step, np.float64)[:, :, :2]  # [steps, 3, (cycles, ticks)]
@@ -284,10 +285,14 @@ def clock_stats(per_step):
         return None
     step = c[:, :, 0].sum(1) / np.maximum(c[:, :, 1].sum(1), 1) * 0.1
     layer = c[:, :, 0].sum(0) / np.maximum(c[:, :, 1].sum(0), 1) * 0.1
-    return {"mean_ghz": round(float(c[..., 0].sum() / c[..., 1].sum() * 0.1), 4),
-            "min_ghz": round(float(step.min()), 4), "max_ghz": round(float(step.max()), 4),
-            "per_layer_ghz": [round(float(x), 4) for x in layer], "steps": len(per_step),
-            "stamped_ms": round(float(c[..., 1].sum() / 1e5), 1)}
+    out = {"mean_ghz": round(float(c[..., 0].sum() / c[..., 1].sum() * 0.1), 4),
+           "per_layer_ghz": [round(float(x), 4) for x in layer], "steps": steps or len(per_step),
+           "stamped_ms": round(float(c[..., 1].sum() / 1e5), 1)}
+    if len(per_step) > 1:
+        out.update(min_ghz=round(float(step.min()), 4), max_ghz=round(float(step.max()), 4))
+    else:
+        out["read"] = "once, summed over the timed steps"
+    return out
 
 
 def wave_slot_occupancy(per_step, slots):
@@ -499,21 +504,22 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    # shader clock of every timed step from libpst's clock counters (pst_clock_counters: stamps
-    # of the fused MPNN launches), read between steps, outside each step's own timing
+    # shader clock of the timed steps from libpst's clock counters (pst_clock_counters: stamps of
+    # the fused MPNN launches, enabled for the bench only), read once after the timed loop so the
+    # bracketed time holds no instrumentation
+    tk.set_clock_counters(True)
     tk.clock_counters(reset=True)
-    times, clk = [], []
+    times = []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         t0 = time.perf_counter()
         tok, nt, nn = tk.tokenize_packed(ppos, pflags, off)  # host → host, synchronous
         times.append(time.perf_counter() - t0)
-        clk.append(tk.clock_counters(reset=True))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    clock = clock_stats(clk)
+    clock = clock_stats([tk.clock_counters(reset=True)], steps=args.steps)
     plan = tk.last_plan_detail()  # chunks and layer schedule of the timed step (rank 0's share)
     log(f"rank {rank}: {args.steps} timed steps in {elapsed:.2f} s")
     stats = torch.tensor(times + [elapsed], dtype=torch.float64, device=red_dev)
@@ -584,18 +590,15 @@ def main():
     occupancy = wave_slot_occupancy(sclk, 8 * torch.cuda.get_device_properties(dev).multi_processor_count)
     stage = {k: v / 3 for k, v in stage.items()}
     tk.set_timing(False)
+    tk.set_clock_counters(False)
 
     kern = {}
-    # layers 1-2 as one launch (k_mpnn_x, PST_MPNN_XLAYER): its time lands in stage mpnn2
-    xlayer = stage["mpnn1"] < 0.05 * stage["mpnn2"]
-    groups = (("mpnn0", ("mpnn0",)), ("mpnn12", ("mpnn1", "mpnn2"))) if xlayer else \
-        tuple((n, (n,)) for n in ("mpnn0", "mpnn1", "mpnn2"))
-    for name, parts in groups:
-        ms = sum(stage[p] for p in parts)
-        ex = sum(MFMA_PER_TASK[p] for p in parts) * MFMA_FLOP * (R / 32) / (ms * 1e-3) / 1e12
+    for name in ("mpnn0", "mpnn1", "mpnn2"):
+        ms = stage[name]
+        ex = MFMA_PER_TASK[name] * MFMA_FLOP * (R / 32) / (ms * 1e-3) / 1e12
         kern[name] = {"launch_ms": round(ms, 3), "executed_mfma_tflops": round(ex, 2),
                       "frac": round(ex / PEAK_FP32_TFLOPS, 4)}
-    dom = "mpnn12" if xlayer else "mpnn1"
+    dom = "mpnn1"
     dom_ms = kern[dom]["launch_ms"]
     executed = kern[dom]["executed_mfma_tflops"]
     traffic = None
@@ -608,8 +611,7 @@ def main():
                    "achieved_GBps": round(per_res * R / (dom_ms * 1e-3) / 1e9, 1),
                    "source": tf.get("source", args.traffic_file)}
     roofline = {
-        "kernel": ("k_mpnn_x (layers 1-2 as one persistent queue)" if xlayer else
-                   "k_mpnn<1> (edge MLP L1 + message MLP L2 + node FFN, fused)"),
+        "kernel": "k_mpnn<1> (edge MLP L1 + message MLP L2 + node FFN, fused)",
         "bound": "mfma", "achieved": executed, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": round(executed / PEAK_FP32_TFLOPS, 4),
         "traffic": traffic["bytes_per_launch"] if traffic else None,  # HBM bytes per launch (PMC)
@@ -618,7 +620,7 @@ def main():
                 "SQ_INSTS_MFMA) / HIP-event launch time; effective_alg_tflops counts SURVEY 8d's algorithmic "
                 "FLOPs instead, which the kernel's algebraic rewrites (DESIGN.md 5) execute in 0.52x the work",
         "launch_ms": round(dom_ms, 3),
-        "effective_alg_tflops": round(MPNN1_ALG_FLOP_PER_RES * (2 if xlayer else 1) * R / (dom_ms * 1e-3) / 1e12, 2),
+        "effective_alg_tflops": round(MPNN1_ALG_FLOP_PER_RES * R / (dom_ms * 1e-3) / 1e12, 2),
         # the peak is quoted at the 2.4 GHz spec clock; at the clock the chip actually held under
         # k_mpnn<1> in the stage-timing steps (its launches' clock stamps) the reachable peak is
         # peak x clock / 2.4

@@ -263,8 +263,11 @@ int pst_get_timing(pst_ctx* ctx, float* ms);
  * of workgroup 0 (clock = out[0] / out[1] x 100 MHz; the persistent queue form's waves live as
  * long as the launch); 2: Σ wave lifetimes (100 MHz ticks); 3 / 4: earliest wave start / latest
  * wave end; 5: waves (occupancy = out[2] / (wave slots x (out[4] - out[3]))); 6, 7: 0. reset != 0
- * restarts them after the read. Split-schedule layers (small batches) add nothing. */
+ * restarts them after the read. Split-schedule layers (small batches) add nothing. The stamps run
+ * only while enabled (pst_set_clock_counters); a context starts with them off, so production
+ * launches carry no measurement code path. */
 int pst_clock_counters(pst_ctx* ctx, uint64_t* out, int32_t reset);
+int pst_set_clock_counters(pst_ctx* ctx, int32_t enable);
 
 /* Stream the context launches on (hipStream_t), for event timing by callers. */
 void* pst_stream(pst_ctx* ctx);

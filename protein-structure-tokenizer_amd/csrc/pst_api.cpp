@@ -43,8 +43,6 @@ constexpr bool MPNN_QUEUE_DEFAULT = true;
 // 1 024 / 512 / 256 proteins 8.24-8.30 / 4.15-4.21 / 2.08-2.09 ms against 8.42 / 4.34-4.37 /
 // 2.12 ms as the queue (profiles/r04_ab_qgroup.txt) — layers 1 and 2 gain from it.
 constexpr int64_t MPNN_QUEUE_LAYERS = 6;
-// Layers 1 and 2 as one persistent launch (k_mpnn_x): layer 2's units fill layer 1's tail.
-constexpr bool MPNN_XLAYER_DEFAULT = false;
 bool use_half_tasks(int64_t n_tasks, int64_t n_simds) { return 2 * n_tasks > n_simds && n_tasks <= n_simds; }
 bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
   const int64_t k = (n_tasks + n_simds - 1) / n_simds;
@@ -261,7 +259,6 @@ struct pst_ctx {
                              // per CU with all of W1 in LDS (k_mpnn<0..2> -1.0..-2.8 %, profiles/r04_ab_qwaves.txt)
   int64_t mpnn_qgroup = -2;  // PST_MPNN_QGROUP: queue unit order, tasks per group (0 = halves adjacent); -1 = wave slots per XCD
   int64_t mpnn_queue_layers = -2;  // PST_MPNN_QUEUE_LAYERS: layer mask of the queue form; -1 = MPNN_QUEUE_LAYERS
-  int64_t mpnn_xlayer = -2;  // PST_MPNN_XLAYER: 1 = layers 1-2 as one persistent queue (k_mpnn_x) when both are queued
   int64_t mpnn_queue = -2;   // PST_MPNN_QUEUE: 1 = fused layers as the half-task queue (k_mpnn_q) whenever not
                              // k_mpnn<L, true>, 0 = never (k_mpnn<L, false>); -1 = policy
   std::vector<int64_t> h_offsets;
@@ -294,6 +291,7 @@ struct pst_ctx {
   // 100 MHz ticks] of the stamping wave, Σ wave lifetimes, min wave start, max wave end, waves —
   // summed over calls (min / max over calls)
   unsigned long long* d_clk = nullptr;
+  bool clock_on = false;  // pst_set_clock_counters: stamp the fused MPNN launches (off by default)
 };
 
 namespace {
@@ -656,9 +654,6 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
   env_threshold(ctx->mpnn_queue_layers, "PST_MPNN_QUEUE_LAYERS");
   const int64_t queue_layers = ctx->mpnn_queue_layers >= 0 ? ctx->mpnn_queue_layers : MPNN_QUEUE_LAYERS;
   if (queue) HIPCHK(hipMemsetAsync(w.qctr, 0, sizeof(int32_t) * 3 * (128 + n_tasks), st));
-  env_threshold(ctx->mpnn_xlayer, "PST_MPNN_XLAYER");
-  const bool xlayer = queue && (queue_layers & 6) == 6 && (ctx->mpnn_xlayer >= 0 ? ctx->mpnn_xlayer != 0 : MPNN_XLAYER_DEFAULT);
-  pst::MpnnArgs m1{};  // layer 1's arguments, launched with layer 2's (xlayer)
   float* msg_rows = nullptr;
   int32_t bpw = 1;
   if (split) {
@@ -688,7 +683,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.msg_rows = msg_rows;
     m.blocks_per_wave = bpw;
     m.half_tasks = half ? 1 : 0;
-    m.clk = ctx->d_clk + 8 * l;
+    m.clk = ctx->clock_on ? ctx->d_clk + 8 * l : nullptr;
     if (queue && ((queue_layers >> l) & 1)) {
       m.q_head = w.qctr + l * (128 + n_tasks);
       m.q_done = m.q_head + 128;
@@ -739,16 +734,8 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.e_out = ebuf[l];
     m.h_out = hbuf[l + 1];
     m.P_out = pbuf[l];
-    if (xlayer && l == 1)
-      m1 = m;  // stage mpnn1 reads ~0, mpnn2 both layers
-    else if (xlayer && l == 2)
-      pst::launch_mpnn_x(m1, m, st);
-    else
-      pst::launch_mpnn(l, m, node_coop, st);
+    pst::launch_mpnn(l, m, node_coop, st);
     mark(ctx, 3 + l);
-    if (xlayer && l == 1) continue;  // layer 1's debug copy follows the joint launch
-    if (xlayer && l == 2 && ctx->dbg[1])
-      HIPCHK(hipMemcpyAsync(ctx->dbg[1], m1.h_out, sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
     if (ctx->dbg[l]) HIPCHK(hipMemcpyAsync(ctx->dbg[l], m.h_out, sizeof(float) * 128 * Rpad, hipMemcpyDeviceToDevice, st));
   }
   // k_down updates the original track in place, so it works on a copy of h3 (h3 stays available
@@ -834,6 +821,12 @@ int pst_get_timing(pst_ctx* ctx, float* ms) {
   if (!ctx || !ctx->timing || !ms) return PST_E_INVALID;
   HIPCHK(hipEventSynchronize(ctx->ev[PST_N_STAGES]));
   for (int i = 0; i < PST_N_STAGES; ++i) HIPCHK(hipEventElapsedTime(&ms[i], ctx->ev[i], ctx->ev[i + 1]));
+  return PST_OK;
+}
+
+int pst_set_clock_counters(pst_ctx* ctx, int32_t enable) {
+  if (!ctx) return PST_E_INVALID;
+  ctx->clock_on = enable != 0;
   return PST_OK;
 }
 

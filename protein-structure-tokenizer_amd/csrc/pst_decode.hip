@@ -39,14 +39,6 @@ namespace dec {
 enum { F_RELU_OUT = 1, F_RELU_IN = 2, F_ACCUM = 4, F_SIGMOID_OUT = 8, F_QSCALE = 16 };
 #define Q_SCALE 0.176776695296637f
 
-__global__ void k_scale(float* x, int64_t n, float s) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[i] = x[i] * s;
-}
-__global__ void k_add(float* x, const float* y, int64_t n) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[i] = x[i] + y[i];
-}
 __global__ void k_zero(float* x, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = 0.0f;
@@ -368,18 +360,6 @@ __global__ __launch_bounds__(256) void k_up_attn(const float* __restrict__ q, co
   }
 }
 
-// P[pair (i, j) of protein b][c] = left[i][c] * right[j][c] (256 channels, einsum "nd,kd->nkd")
-__global__ void k_pair_product(const float* __restrict__ left, const float* __restrict__ right, float* __restrict__ P,
-                               DecBatch bt) {
-  const int64_t pr = blockIdx.x;
-  const int b = pair_protein(bt, pr);
-  const int64_t n0 = bt.node_off[b];
-  const int64_t Nb = bt.node_off[b + 1] - n0, loc = pr - bt.pair_off[b];
-  const int64_t i = n0 + loc / Nb, j = n0 + loc % Nb;
-  const int c = threadIdx.x;
-  P[pr * 256 + c] = left[i * 256 + c] * right[j * 256 + c];
-}
-
 // ---------------------------------------------------------------- fused pair representation
 // The whole per-pair chain of the sequence decoder and the structure module's pair inputs in one
 // pass over 32-pair wave tiles (pst_device.h layout, f32 MFMA), instead of ~12 library GEMMs and
@@ -512,18 +492,6 @@ __global__ __launch_bounds__(256) void k_pair_fused(PairArgs a) {
   }
 }
 
-// C[pair (i, j)] = [PE(j - i; 512) | pair0[pair]] (sequence_decoder.py:69-99)
-__global__ void k_pair_concat(const float* __restrict__ pe_rel /*[1023][128], row = d + 511*/,
-                              const float* __restrict__ pair0, float* __restrict__ C, DecBatch bt) {
-  const int64_t pr = blockIdx.x;
-  const int b = pair_protein(bt, pr);
-  const int64_t Nb = bt.node_off[b + 1] - bt.node_off[b], loc = pr - bt.pair_off[b];
-  const int il = (int)(loc / Nb), jl = (int)(loc % Nb);
-  const int c = threadIdx.x;
-  C[pr * 256 + c] = pe_rel[(int64_t)(jl - il + 511) * 128 + c];
-  C[pr * 256 + 128 + c] = pair0[pr * 128 + c];
-}
-
 // ---------------------------------------------------------------- structure module helpers
 __device__ __forceinline__ void quat_to_rot(const float* q, float* r) {
   // QUAT_TO_ROT contraction (quat_affine.py:43-56, 143-157)
@@ -611,19 +579,18 @@ __global__ void k_ipa_points(const float* __restrict__ qpl /*[N][144]*/, const f
 // The attention weights live in LDS transposed, attT[j][ATT_LD] (heads 0..11 of key j, row
 // stride 13 words: odd, so a wave's 64 consecutive keys of one head hit 32 distinct banks in the
 // softmax, and the MFMA operand reads below conflict at most 2-way).
-// MFMA_PAIR: the pair attention Σ_j att[h][j]·z_ij[c] (12 heads × 128 channels, the largest of
-// the weighted sums) runs on v_mfma_f32_16x16x4_f32 — D[c][h] = Σ_j z[j][c]·att[h][j], wave w
-// owning channels 32w..32w+31 as two 16-row blocks, the 12 heads in columns 0..11 of the 16.
-// That instruction is a k-ascending fmaf chain (tools/probe/mfma_probe.hip: 256/256 bitwise), so
-// every sum is the same in-order chain over j from 0 as the VALU form (!MFMA_PAIR, kept for the
-// A/B test): identical bits. The value sums (480 outputs, one head each) stay on the VALU.
+// The pair attention Σ_j att[h][j]·z_ij[c] (12 heads × 128 channels, the largest of the weighted
+// sums) runs on v_mfma_f32_16x16x4_f32 — D[c][h] = Σ_j z[j][c]·att[h][j], wave w owning channels
+// 32w..32w+31 as two 16-row blocks, the 12 heads in columns 0..11 of the 16. That instruction is
+// a k-ascending fmaf chain (tools/probe/mfma_probe.hip: 256/256 bitwise), so every sum is the
+// in-order chain over j from 0 (round 3 measured it bitwise equal to per-query VALU fmaf chains;
+// that form is tools/variants/decode_ab.patch). The attention weights go to att_out for the
+// value sums (k_ipa_values) and the local frames (k_ipa_local).
 constexpr int ATT_LD = 13;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <bool MFMA_PAIR>
 __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /*[N][192]*/,
-                                                  const float* __restrict__ kvs_all /*[N][384]*/,
-                                                  const float* __restrict__ qpg, const float* __restrict__ kvpg_all,
+                                                  const float* __restrict__ qpg,
                                                   const float* __restrict__ b2d_all /*[pairs][12], × sqrt(1/3)*/,
                                                   const float* __restrict__ zln_all /*[pairs][128]*/,
                                                   const float* __restrict__ pw /*[12]*/,
@@ -631,19 +598,16 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
                                                   float* __restrict__ feat /*[N][2112]*/, DecBatch bt,
                                                   const float* __restrict__ kT_all /*[192][Ntot]*/,
                                                   const float* __restrict__ kpT_all /*[144][Ntot]*/, int Ntot,
-                                                  int ld /*row stride of qs and kvs*/,
-                                                  float* __restrict__ att_out /*[pairs][12] or null*/) {
+                                                  int ld /*row stride of qs*/,
+                                                  float* __restrict__ att_out /*[pairs][12]*/) {
   __shared__ float attT[512 * ATT_LD];
-  __shared__ float res_pt[12 * 8 * 3];
   const int64_t ig = blockIdx.x;
   const int tid = threadIdx.x;
   const int bprot = bt.node_prot[ig];
   const int64_t n0 = bt.node_off[bprot];
   const int N = (int)(bt.node_off[bprot + 1] - n0);
   const int il = (int)(ig - n0);
-  // protein-local views: rows j of kvs/kvpg, pair rows (il, j) of b2d/zln
-  const float* kvs = kvs_all + n0 * ld;
-  const float* kvpg = kvpg_all + n0 * 432;
+  // protein-local views: pair rows (il, j) of b2d/zln
   const float* b2d = b2d_all + (bt.pair_off[bprot] + (int64_t)il * N) * 12;
   const float* zln = zln_all + (bt.pair_off[bprot] + (int64_t)il * N) * 128;
   const float sw = 0.144337567297406f;  // sqrt(1 / (3 * 16))
@@ -705,12 +669,11 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
   }
   __syncthreads();
   float* f = feat + ig * 2112;
-  if (MFMA_PAIR && att_out) {
+  {
     // the attention weights of query i for k_ipa_values: att_out[(pair row (i, j)) * 12 + h]
     float* ao = att_out + (bt.pair_off[bprot] + (int64_t)il * N) * 12;
     for (int e = tid; e < N * 12; e += 256) ao[e] = attT[(e / 12) * ATT_LD + e % 12];
   }
-  if (MFMA_PAIR)
   {
     // pair attention on the matrix cores: lane (i = lane & 15, g = lane >> 4) feeds A = z[4s+g][c0+i]
     // and B = att[head i][4s+g] (0 for the 4 padding heads); after the chain it holds
@@ -754,94 +717,6 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
       *reinterpret_cast<float4*>(o + 16) = make_float4(accB[0], accB[1], accB[2], accB[3]);
     }
   }
-  if (MFMA_PAIR && att_out) return;  // value sums and the local frames: k_ipa_values, k_ipa_local
-  // Value sums (and, without MFMA_PAIR, the pair attention): per thread the value outputs
-  // o = tid and tid + 256 (scalar values 0..191, global value points 192..479) and, VALU form, the
-  // pair attention of channel c for heads hg, hg+2, ... (6 sums). Each sum is its own in-order
-  // fmaf chain over j; loads run 8 keys ahead.
-  {
-    const int c = tid & 127, hg = tid >> 7;
-    const float* zr = zln + c;
-    const float* vsrc[2];
-    int64_t vstride[2];
-    int vh[2];
-    bool vok[2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int o = tid + 256 * m;
-      vok[m] = o < 192 + 288;
-      if (o < 192) {
-        vh[m] = o / 16;
-        vsrc[m] = kvs + vh[m] * 32 + 16 + o % 16;
-        vstride[m] = ld;
-      } else {
-        const int q = vok[m] ? o - 192 : 0;
-        vh[m] = q / 24;
-        vsrc[m] = kvpg + (vh[m] * 12 + 4 + (q / 3) % 8) * 3 + q % 3;
-        vstride[m] = 432;
-      }
-    }
-    float pacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float vacc[2] = {0.f, 0.f};
-    int j = 0;
-    for (; j + 8 <= N; j += 8) {
-      float zv[8], v0[8], v1[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (!MFMA_PAIR) zv[u] = zr[(int64_t)(j + u) * 128];
-        v0[u] = vsrc[0][(int64_t)(j + u) * vstride[0]];
-        v1[u] = vok[1] ? vsrc[1][(int64_t)(j + u) * vstride[1]] : 0.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (!MFMA_PAIR) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) pacc[k] = __builtin_fmaf(attT[(j + u) * ATT_LD + hg + 2 * k], zv[u], pacc[k]);
-        }
-        vacc[0] = __builtin_fmaf(attT[(j + u) * ATT_LD + vh[0]], v0[u], vacc[0]);
-        vacc[1] = __builtin_fmaf(attT[(j + u) * ATT_LD + vh[1]], v1[u], vacc[1]);
-      }
-    }
-    for (; j < N; ++j) {
-      if (!MFMA_PAIR) {
-        const float zv = zr[(int64_t)j * 128];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) pacc[k] = __builtin_fmaf(attT[j * ATT_LD + hg + 2 * k], zv, pacc[k]);
-      }
-      vacc[0] = __builtin_fmaf(attT[j * ATT_LD + vh[0]], vsrc[0][(int64_t)j * vstride[0]], vacc[0]);
-      if (vok[1]) vacc[1] = __builtin_fmaf(attT[j * ATT_LD + vh[1]], vsrc[1][(int64_t)j * vstride[1]], vacc[1]);
-    }
-    if (!MFMA_PAIR) {
-#pragma unroll
-      for (int u = 0; u < 6; ++u) f[576 + (hg + 2 * u) * 128 + c] = pacc[u];
-    }
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int o = tid + 256 * m;
-      if (!vok[m]) continue;
-      if (o < 192)
-        f[o] = vacc[m];
-      else
-        res_pt[o - 192] = vacc[m];
-    }
-  }
-  __syncthreads();
-  // global → local frame of i (invert_point) and norms
-  if (tid < 96) {
-    const int h = tid / 8, p = tid % 8;
-    const float* R = rot + ig * 9;
-    const float* tr = aff + ig * 7 + 4;
-    const float gx = res_pt[(h * 8 + p) * 3 + 0] - tr[0];
-    const float gy = res_pt[(h * 8 + p) * 3 + 1] - tr[1];
-    const float gz = res_pt[(h * 8 + p) * 3 + 2] - tr[2];
-    const float lx = R[0] * gx + R[3] * gy + R[6] * gz;
-    const float ly = R[1] * gx + R[4] * gy + R[7] * gz;
-    const float lz = R[2] * gx + R[5] * gy + R[8] * gz;
-    f[192 + tid] = lx;
-    f[288 + tid] = ly;
-    f[384 + tid] = lz;
-    f[480 + tid] = sqrtf(((1e-8f + lx * lx) + ly * ly) + lz * lz);
-  }
 }
 
 // IPA value sums, batched over queries (the per-query form re-read every key's values from L2:
@@ -849,7 +724,7 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
 // D[q][o] = Σ_j att[q][h][j] · V_h[j][o] on v_mfma_f32_16x16x4_f32 for the 16 scalar values and
 // the 8 value points × xyz (24) of head h — three 16-wide output blocks (8 columns unused). The
 // instruction is a k-ascending fmaf chain, so each sum is the in-order chain over j from 0 that
-// k_ipa_attn<false> runs per query: identical bits. Scalar outputs go to feat[q][16h + o], the
+// a per-query VALU loop would run: identical bits. Scalar outputs go to feat[q][16h + o], the
 // global-frame points to vpt[q][24h + o'] for k_ipa_local.
 __global__ __launch_bounds__(64) void k_ipa_values(const float* __restrict__ att_all, const float* __restrict__ kvs_all,
                                                    const float* __restrict__ kvpg_all, float* __restrict__ feat,
@@ -1514,15 +1389,8 @@ inline void gemm_any(hipStream_t st, const float* X, int ldx, const float* Wt, i
       const dim3 grid((unsigned)(((N + 32 * nacc - 1) / (32 * nacc)) * ((M + 31) / 32)));  // 1-D, XCD-aware in the kernel
       hipLaunchKernelGGL(kern, grid, dim3(64 * slices), 0, st, X, ldx, Wt, N, b, Y, ldy, M, N, K, flags, ks);
     };
-    if (K >= 1024) {  // the IPA output projection (K = 2112): NACC column tiles per wave re-read X less
-      static const int nacc = getenv("PST_DECODE_WIDE_NACC") ? atoi(getenv("PST_DECODE_WIDE_NACC")) : 1;
-      if (nacc == 4 && N % 128 == 0)
-        go(k_gemm_mfma<16, 4>, 16, 4);
-      else if (nacc == 2 && N % 64 == 0)
-        go(k_gemm_mfma<16, 2>, 16, 2);
-      else
-        go(k_gemm_mfma<16, 1>, 16);
-    }
+    if (K >= 1024)  // the IPA output projection (K = 2112); 2 or 4 column tiles per wave: no gain (round 4)
+      go(k_gemm_mfma<16, 1>, 16);
     else if (K >= 256)
       go(k_gemm_mfma<8, 1>, 8);
     else
@@ -1552,10 +1420,10 @@ constexpr int64_t kNodeCap = 8192;
 constexpr int64_t kPairCap = int64_t(1) << 20;
 
 struct Scratch {
-  float *orig_in, *orig, *res, *ln_a, *ln_b, *q, *k, *v, *gate, *wavg, *tr_h;
-  float *left, *right, *P, *h1, *pair0, *catb, *lin_out, *lnz, *z, *zln, *b2d;
-  float *single_ln, *act, *init_act, *act_ln, *tmp384a, *tmp384b, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
-  float *aff, *rot, *sca, *scb, *sct, *unnorm, *angles, *traj, *atom37, *atom14, *kT, *kpT, *init_relu, *ipa_in;
+  float *orig_in, *orig, *res, *ln_a, *q, *k, *v, *gate, *wavg;
+  float *left, *right, *z, *zln, *b2d;
+  float *act, *init_act, *qs, *kvs, *qpl, *kvpl, *qpg, *kvpg, *feat, *upd;
+  float *aff, *rot, *unnorm, *angles, *traj, *atom37, *atom14, *kT, *kpT, *init_relu, *ipa_in;
   int64_t *tok_off, *node_off, *pair_off;
   int32_t *tok_prot, *node_prot, *vt_prot, *vt_q0;
   float *att, *vpt;
@@ -1570,20 +1438,15 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
   };
   const size_t F = sizeof(float);
   It items[] = {{(void**)&S->orig_in, NN * 256 * F}, {(void**)&S->orig, NN * 128 * F}, {(void**)&S->res, NN * 128 * F},
-                {(void**)&S->ln_a, NN * 128 * F},    {(void**)&S->ln_b, NN * 128 * F}, {(void**)&S->q, NN * 128 * F},
+                {(void**)&S->ln_a, NN * 128 * F},    {(void**)&S->q, NN * 128 * F},
                 {(void**)&S->k, NN * 128 * F},       {(void**)&S->v, NN * 128 * F},    {(void**)&S->gate, NN * 128 * F},
-                {(void**)&S->wavg, NN * 128 * F},    {(void**)&S->tr_h, NN * 256 * F}, {(void**)&S->left, NN * 256 * F},
-                {(void**)&S->right, NN * 256 * F},   {(void**)&S->P, NP * 256 * F},    {(void**)&S->h1, NP * 256 * F},
-                {(void**)&S->pair0, NP * 128 * F},   {(void**)&S->catb, NP * 256 * F}, {(void**)&S->lin_out, NP * 128 * F},
-                {(void**)&S->lnz, NP * 128 * F},     {(void**)&S->z, NP * 128 * F},    {(void**)&S->zln, NP * 128 * F},
-                {(void**)&S->b2d, NP * 12 * F},      {(void**)&S->single_ln, NN * 128 * F},
-                {(void**)&S->act, NN * 384 * F},     {(void**)&S->init_act, NN * 128 * F},
-                {(void**)&S->act_ln, NN * 384 * F},  {(void**)&S->tmp384a, NN * 384 * F},
-                {(void**)&S->tmp384b, NN * 384 * F}, {(void**)&S->ipa_in, NN * 1152 * F},
+                {(void**)&S->wavg, NN * 128 * F},    {(void**)&S->left, NN * 256 * F},
+                {(void**)&S->right, NN * 256 * F},   {(void**)&S->z, NP * 128 * F},    {(void**)&S->zln, NP * 128 * F},
+                {(void**)&S->b2d, NP * 12 * F},      {(void**)&S->act, NN * 384 * F},     {(void**)&S->init_act, NN * 128 * F},
+                {(void**)&S->ipa_in, NN * 1152 * F},
                 {(void**)&S->qpg, NN * 144 * F},
                 {(void**)&S->kvpg, NN * 432 * F},    {(void**)&S->feat, NN * 2112 * F}, {(void**)&S->upd, NN * 6 * F},
-                {(void**)&S->aff, NN * 7 * F},       {(void**)&S->rot, NN * 9 * F},    {(void**)&S->sca, NN * 128 * F},
-                {(void**)&S->scb, NN * 128 * F},     {(void**)&S->sct, NN * 128 * F},  {(void**)&S->unnorm, NN * 6 * F},
+                {(void**)&S->aff, NN * 7 * F},       {(void**)&S->rot, NN * 9 * F},    {(void**)&S->unnorm, NN * 6 * F},
                 {(void**)&S->angles, 8 * NN * 6 * F}, {(void**)&S->traj, 8 * NN * 7 * F},
                 {(void**)&S->atom37, NN * 111 * F},  {(void**)&S->atom14, NN * 42 * F},
                 {(void**)&S->kT, NN * 192 * F}, {(void**)&S->kpT, NN * 144 * F},
@@ -1675,10 +1538,6 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   }
   DecBatch bt{G.B, S.tok_off, S.node_off, S.pair_off, S.tok_prot, S.node_prot};
   const int Ni = (int)N;
-  const bool fused = !getenv("PST_DECODE_UNFUSED");
-  const bool ipa_mfma = !getenv("PST_DECODE_IPA_VALU");  // A/B: the VALU pair sum (same bits)
-  // the fold iteration's tail as one fused launch (PST_DECODE_UNFUSED_TAIL=1: the 13 launches)
-  const bool fold_tail = !getenv("PST_DECODE_UNFUSED_TAIL");
   auto launch = [&]() -> int {
     // ---- upsampler (CrossAttentionScaler, use_original_posenc)
     hipLaunchKernelGGL(k_up_init, dim3((unsigned)T), dim3(128), 0, st, S.tokens, bt, T, dec->d_levels, dec->D,
@@ -1686,76 +1545,38 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     gemm(st, S.orig_in, 256, W.proj_original, S.orig, 128, (int)T, 0);
     hipLaunchKernelGGL(k_node_pe, dim3((unsigned)N), dim3(128), 0, st, dec->d_pe_node, bt, N, S.res);
     for (int b = 0; b < 3; ++b) {
-      if (fold_tail) {  // LayerNorm + both projections per operand in one launch (k_ln_proj2)
-        LnProj2Args qa{S.res, Ni, W.qn[b].s, W.qn[b].o, {W.wq[b], W.wg[b]}, {nullptr, W.gb[b]},
-                       {F_QSCALE, F_SIGMOID_OUT}, {S.q, S.gate}};
-        hipLaunchKernelGGL(k_ln_proj2, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, qa);
-        LnProj2Args ka{S.orig, (int)T, W.dn[b].s, W.dn[b].o, {W.wk[b], W.wv[b]}, {nullptr, nullptr}, {0, 0},
-                       {S.k, S.v}};
-        hipLaunchKernelGGL(k_ln_proj2, dim3((unsigned)((T + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, ka);
-      } else {
-      layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.qn[b]);
-      layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.dn[b]);
-      gemm_raw(st, S.ln_a, 128, W.wq[b], 128, 128, nullptr, S.q, 128, Ni, F_QSCALE);  // q · key_dim^-0.5
-      gemm_raw(st, S.ln_a, 128, W.wg[b], 128, 128, W.gb[b], S.gate, 128, Ni, F_SIGMOID_OUT);
-      gemm_raw(st, S.ln_b, 128, W.wk[b], 128, 128, nullptr, S.k, 128, (int)T, 0);
-      gemm_raw(st, S.ln_b, 128, W.wv[b], 128, 128, nullptr, S.v, 128, (int)T, 0);
-      }
+      // LayerNorm + both projections per operand in one launch (k_ln_proj2; q · key_dim^-0.5)
+      LnProj2Args qa{S.res, Ni, W.qn[b].s, W.qn[b].o, {W.wq[b], W.wg[b]}, {nullptr, W.gb[b]},
+                     {F_QSCALE, F_SIGMOID_OUT}, {S.q, S.gate}};
+      hipLaunchKernelGGL(k_ln_proj2, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, qa);
+      LnProj2Args ka{S.orig, (int)T, W.dn[b].s, W.dn[b].o, {W.wk[b], W.wv[b]}, {nullptr, nullptr}, {0, 0},
+                     {S.k, S.v}};
+      hipLaunchKernelGGL(k_ln_proj2, dim3((unsigned)((T + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, ka);
       hipLaunchKernelGGL(k_up_attn, dim3((unsigned)N), dim3(256), 0, st, S.q, S.k, S.v, S.gate, S.wavg, bt, N);
       gemm_raw(st, S.wavg, 128, W.wo[b], 128, 128, W.ob[b], S.res, 128, Ni, F_ACCUM);
-      if (fold_tail) {  // the two Transitions fused (k_transition128), same gating as k_fold_tail
-        Trans128Args ta{S.res, Ni, W.rt_ln[b].s, W.rt_ln[b].o, W.rt1[b].w, W.rt1[b].b, W.rt2[b].w, W.rt2[b].b};
-        hipLaunchKernelGGL(k_transition128, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, ta);
-        Trans128Args tb{S.orig, (int)T, W.ot_ln[b].s, W.ot_ln[b].o, W.ot1[b].w, W.ot1[b].b, W.ot2[b].w, W.ot2[b].b};
-        hipLaunchKernelGGL(k_transition128, dim3((unsigned)((T + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, tb);
-      } else {
-      layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.rt_ln[b]);
-      gemm(st, S.ln_a, 128, W.rt1[b], S.tr_h, 256, Ni, F_RELU_OUT);
-      gemm(st, S.tr_h, 256, W.rt2[b], S.res, 128, Ni, F_ACCUM);
-      layernorm(st, S.orig, 128, S.ln_b, 128, (int)T, 128, W.ot_ln[b]);
-      gemm(st, S.ln_b, 128, W.ot1[b], S.tr_h, 256, (int)T, F_RELU_OUT);
-      gemm(st, S.tr_h, 256, W.ot2[b], S.orig, 128, (int)T, F_ACCUM);
-      }
+      // the two Transitions fused (k_transition128)
+      Trans128Args ta{S.res, Ni, W.rt_ln[b].s, W.rt_ln[b].o, W.rt1[b].w, W.rt1[b].b, W.rt2[b].w, W.rt2[b].b};
+      hipLaunchKernelGGL(k_transition128, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, ta);
+      Trans128Args tb{S.orig, (int)T, W.ot_ln[b].s, W.ot_ln[b].o, W.ot1[b].w, W.ot1[b].b, W.ot2[b].w, W.ot2[b].b};
+      hipLaunchKernelGGL(k_transition128, dim3((unsigned)((T + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, tb);
     }
     hipLaunchKernelGGL(k_spherical, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.res, Ni);  // s_i
     // ---- sequence decoder: pair representation over each protein's N_b² pairs
-    const int NPi = (int)NP;
     layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.pr_ln_in);
     gemm(st, S.ln_a, 128, W.left, S.left, 256, Ni, 0);
     gemm(st, S.ln_a, 128, W.right, S.right, 256, Ni, 0);
-    if (fused) {
-      layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
-      gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
-      PairArgs pa = dec->pair;
-      pa.left = S.left;
-      pa.right = S.right;
-      pa.z = keep_debug ? S.z : nullptr;
-      pa.zln = S.zln;
-      pa.b2d = S.b2d;
-      pa.NP = NP;
-      pa.bt = bt;
-      const int64_t tiles = (NP + 31) / 32;
-      hipLaunchKernelGGL(k_pair_fused, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, pa);
-    } else {
-      hipLaunchKernelGGL(k_pair_product, dim3((unsigned)NP), dim3(256), 0, st, S.left, S.right, S.P, bt);
-      gemm(st, S.P, 256, W.out1, S.h1, 256, NPi, F_RELU_OUT);
-      gemm(st, S.h1, 256, W.out2, S.pair0, 128, NPi, 0);
-      gemm(st, S.P, 256, W.right1, S.lin_out, 128, NPi, 0);
-      hipLaunchKernelGGL(k_add, dim3((unsigned)((NP * 128 + 255) / 256)), dim3(256), 0, st, S.pair0, S.lin_out, NP * 128);
-      layernorm(st, S.pair0, 128, S.pair0, 128, NPi, 128, W.pr_ln_out);
-      hipLaunchKernelGGL(k_pair_concat, dim3((unsigned)NP), dim3(128), 0, st, dec->d_pe_rel, S.pair0, S.catb, bt);
-      gemm(st, S.catb, 256, W.seq_linear, S.lin_out, 128, NPi, 0);
-      layernorm(st, S.lin_out, 128, S.lnz, 128, NPi, 128, W.pt_ln);
-      gemm(st, S.lnz, 128, W.pt1, S.h1, 256, NPi, F_RELU_OUT);
-      gemm(st, S.h1, 256, W.pt2, S.z, 128, NPi, 0);  // z_ij (Transition output, no residual)
-      // ---- structure module
-      layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
-      gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
-      layernorm(st, S.z, 128, S.zln, 128, NPi, 128, W.pair_ln);
-      gemm(st, S.zln, 128, W.att2d, S.b2d, 12, NPi, 0);
-      hipLaunchKernelGGL(k_scale, dim3((unsigned)((NP * 12 + 255) / 256)), dim3(256), 0, st, S.b2d, NP * 12,
-                         0.577350269189626f);
-    }
+    layernorm(st, S.res, 128, S.init_act, 128, Ni, 128, W.single_ln);
+    gemm(st, S.init_act, 128, W.init_proj, S.act, 384, Ni, 0);
+    PairArgs pa = dec->pair;
+    pa.left = S.left;
+    pa.right = S.right;
+    pa.z = keep_debug ? S.z : nullptr;
+    pa.zln = S.zln;
+    pa.b2d = S.b2d;
+    pa.NP = NP;
+    pa.bt = bt;
+    const int64_t tiles = (NP + 31) / 32;
+    hipLaunchKernelGGL(k_pair_fused, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, pa);
     hipLaunchKernelGGL(k_affine_init, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, Ni);
     // relu(init_act) feeds the angle resnet of every iteration: once, not 8 copies
     hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.init_act, 128, S.init_relu,
@@ -1766,43 +1587,19 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
       gemm_raw(st, S.act, 384, dec->d_ipa_w, 384, 1152, dec->d_ipa_b, S.ipa_in, 1152, Ni, 0);
       hipLaunchKernelGGL(k_ipa_points, dim3((unsigned)N), dim3(192), 0, st, S.qpl, S.kvpl, S.aff, S.rot, S.qpg, S.kvpg,
                          S.kvs, S.kT, S.kpT, Ni, 1152);
-      hipLaunchKernelGGL(ipa_mfma ? k_ipa_attn<true> : k_ipa_attn<false>, dim3((unsigned)N), dim3(256), 0, st, S.qs,
-                         S.kvs, S.qpg, S.kvpg, S.b2d, S.zln, dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152,
-                         ipa_mfma ? S.att : nullptr);
-      if (ipa_mfma) {
-        hipLaunchKernelGGL(k_ipa_values, dim3((unsigned)n_vt, 12), dim3(64), 0, st, S.att, S.kvs, S.kvpg, S.feat, S.vpt,
-                           bt, S.vt_prot, S.vt_q0, 1152);
-        hipLaunchKernelGGL(k_ipa_local, dim3((unsigned)N), dim3(96), 0, st, S.vpt, S.aff, S.rot, S.feat, Ni);
-      }
+      hipLaunchKernelGGL(k_ipa_attn, dim3((unsigned)N), dim3(256), 0, st, S.qs, S.qpg, S.b2d, S.zln,
+                         dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152, S.att);
+      hipLaunchKernelGGL(k_ipa_values, dim3((unsigned)n_vt, 12), dim3(64), 0, st, S.att, S.kvs, S.kvpg, S.feat, S.vpt,
+                         bt, S.vt_prot, S.vt_q0, 1152);
+      hipLaunchKernelGGL(k_ipa_local, dim3((unsigned)N), dim3(96), 0, st, S.vpt, S.aff, S.rot, S.feat, Ni);
       gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
-      if (fold_tail) {  // the rest of the iteration's linears and norms in one launch (k_fold_tail)
-        FoldTailArgs ft{S.act, S.init_relu, S.upd, S.unnorm, Ni, W.att_ln.s, W.att_ln.o, W.tr_ln.s, W.tr_ln.o,
-                        {W.tr[0].w, W.tr[1].w, W.tr[2].w}, {W.tr[0].b, W.tr[1].b, W.tr[2].b},
-                        W.affine_update.w, W.affine_update.b, W.sc_in.w, W.sc_in.b, W.sc_in1.w, W.sc_in1.b,
-                        {W.rb1.w, W.rb2.w, W.rb1_1.w, W.rb2_1.w}, {W.rb1.b, W.rb2.b, W.rb1_1.b, W.rb2_1.b},
-                        W.angles.w, W.angles.b};
-        hipLaunchKernelGGL(k_fold_tail, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(64 * FT_WAVES), 0, st, ft);
-      } else {
-      layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.att_ln);
-      gemm(st, S.act, 384, W.tr[0], S.tmp384a, 384, Ni, F_RELU_OUT);
-      gemm(st, S.tmp384a, 384, W.tr[1], S.tmp384b, 384, Ni, F_RELU_OUT);
-      gemm(st, S.tmp384b, 384, W.tr[2], S.act, 384, Ni, F_ACCUM);  // += input_act
-      layernorm(st, S.act, 384, S.act, 384, Ni, 384, W.tr_ln);
-      // the affine update (pre_compose with S.upd) runs at the head of k_sc_geom: nothing between
-      // here and there reads the frames
-      gemm(st, S.act, 384, W.affine_update, S.upd, 6, Ni, 0);
-      // MultiRigidSidechain: (0 + Lin(relu(act))) + Lin(relu(initial_act)), 2 residual blocks, angles;
-      // the first GEMM writes instead of accumulating onto zeros (0 + v == v up to the sign of a zero)
-      gemm(st, S.act, 384, W.sc_in, S.sca, 128, Ni, F_RELU_IN);
-      gemm(st, S.init_relu, 128, W.sc_in1, S.sca, 128, Ni, F_ACCUM);
-      // scb is only ever read through a ReLU: apply it in the producing GEMM's epilogue instead of
-      // as a copy before the consumer (same values)
-      gemm(st, S.sca, 128, W.rb1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
-      gemm(st, S.scb, 128, W.rb2, S.sca, 128, Ni, F_ACCUM);
-      gemm(st, S.sca, 128, W.rb1_1, S.scb, 128, Ni, F_RELU_IN | F_RELU_OUT);
-      gemm(st, S.scb, 128, W.rb2_1, S.sca, 128, Ni, F_ACCUM);
-      gemm(st, S.sca, 128, W.angles, S.unnorm, 6, Ni, F_RELU_IN);
-      }
+      // the rest of the iteration's linears and norms in one launch (k_fold_tail)
+      FoldTailArgs ft{S.act, S.init_relu, S.upd, S.unnorm, Ni, W.att_ln.s, W.att_ln.o, W.tr_ln.s, W.tr_ln.o,
+                      {W.tr[0].w, W.tr[1].w, W.tr[2].w}, {W.tr[0].b, W.tr[1].b, W.tr[2].b},
+                      W.affine_update.w, W.affine_update.b, W.sc_in.w, W.sc_in.b, W.sc_in1.w, W.sc_in1.b,
+                      {W.rb1.w, W.rb2.w, W.rb1_1.w, W.rb2_1.w}, {W.rb1.b, W.rb2.b, W.rb1_1.b, W.rb2_1.b},
+                      W.angles.w, W.angles.b};
+      hipLaunchKernelGGL(k_fold_tail, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(64 * FT_WAVES), 0, st, ft);
       const bool last = it == 7;
       hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.upd, S.unnorm,
                          S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7, last ? S.atom37 : nullptr,
@@ -1821,7 +1618,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     int rc = launch();
     if (rc) return rc;
   } else {
-    std::vector<int64_t> key{(int64_t)t_mfma, (int64_t)fused, (int64_t)ipa_mfma, (int64_t)fold_tail, G.B};
+    std::vector<int64_t> key{(int64_t)t_mfma, G.B};
     key.insert(key.end(), G.node_off.begin(), G.node_off.end());
     key.insert(key.end(), G.tok_off.begin(), G.tok_off.end());
     auto it = dec->graphs.find(key);

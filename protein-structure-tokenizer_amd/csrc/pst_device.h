@@ -380,6 +380,9 @@ __device__ __forceinline__ void tile_store_blk(const Tile& t, float* __restrict_
 #ifndef ACT_GROUP
 #define ACT_GROUP 4
 #endif
+// ActGelu's non-FRESH asm form (k-steps t >= ACT_GROUP) reads accumulators without hazard checks:
+// it relies on their MFMA group having finished at least 4 k-steps earlier, so ACT_GROUP >= 4
+static_assert(ACT_GROUP >= 4 && ACT_GROUP % 2 == 0 && 64 % ACT_GROUP == 0, "ACT_GROUP: even divisor of 64, >= 4");
 template <typename F>
 __device__ __forceinline__ void tile_gemm_f(Tile& acc, const Tile& X, const float4* __restrict__ Wf, F&& f) {
   constexpr int G = ACT_GROUP, NP = G / 2;

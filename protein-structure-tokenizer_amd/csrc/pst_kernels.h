@@ -166,9 +166,6 @@ void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st);
 void launch_knn(const KnnArgs& a, hipStream_t st);
 // node_coop (split schedule only): node update as k_mpnn_node_coop, four waves per 32 receivers
 void launch_mpnn(int layer, const MpnnArgs& a, bool node_coop, hipStream_t st);
-// layers 1 and 2 as one persistent queue (k_mpnn_x; both args queue-form, q_head[120] of a1 counts
-// layer 1's finished tasks)
-void launch_mpnn_x(const MpnnArgs& a1, const MpnnArgs& a2, hipStream_t st);
 // coop (df 1 only): one workgroup per tile, the GEMMs split over its four waves (small batches)
 // downsampler forms (df 1; df 2/4 always run k_down<df>): one wave per tile (k_down<1>), four
 // waves per tile (k_down_coop), two waves per tile, one track each (k_down_pair). Identical bits.

@@ -671,25 +671,9 @@ __device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, 
 // The edge phase of one fused-layer task (receivers task*32 .. task*32+31), edge blocks blk_lo ..
 // blk_hi-1 in order: edge update / embedding, message MLP, and the ordered segment sums of the
 // receivers these blocks complete, stored to agg (perm rows). lds_scratch[w]: this wave's LDS tile.
-// Cross-layer dependency wait (k_mpnn_x): spin until the previous layer's counter of every lane's
-// task t_lane reads 3 (both halves and the node update done, each released at agent scope before
-// its add), then acquire. Bounded: after ~2^22 sleeps the wave stops waiting (its results would
-// then be wrong and the parity tests say so; the kernel still drains instead of hanging the GPU).
-__device__ __forceinline__ void wait_tasks_done(const int32_t* done, int64_t t_lane) {
-  for (int spin = 0; spin < (1 << 22); ++spin) {
-    const int v = __hip_atomic_load(done + t_lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__ballot(v < 3) == 0) break;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
-// dep (k_mpnn_x, previous layer still running): before each block, wait for the previous layer's
-// node updates of the block's sender tasks (their projection rows P_in)
 template <int LAYER, int KL, int NW>
 __device__ __forceinline__ void mpnn_edge_blocks(const MpnnArgs& a, int64_t task, int lane, int blk_lo, int blk_hi,
-                                                 const float4* w1_lds, float (&lds_scratch)[NW][64 * 36], int w,
-                                                 const int32_t* dep = nullptr) {
+                                                 const float4* w1_lds, float (&lds_scratch)[NW][64 * 36], int w) {
   const int64_t g0 = task * 32;
   float* scratch = lds_scratch[w];
   float* aggl = a.agg + task * 32 * 128;
@@ -699,7 +683,6 @@ __device__ __forceinline__ void mpnn_edge_blocks(const MpnnArgs& a, int64_t task
   for (int blk = blk_lo; blk < blk_hi; ++blk) {
     const int32_t s_cur = s_next;
     if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
-    if (dep) wait_tasks_done(dep, s_cur >> 5);
     Tile m;
     edge_block<LAYER, KL>(a, task, g0, lane, blk, s_cur, m, w1_lds);
     // ordered segment sum over the 50 slots of each receiver (jax.ops.segment_sum order). The
@@ -1077,123 +1060,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_mpnn_q(MpnnArgs a_in) {
     }
   }
   cs.stop(a_k->clk);
-}
-
-// Unit j of XCD queue q (k_mpnn_q's order): false when j is past the queue's end
-__device__ __forceinline__ bool queue_unit(const MpnnArgs& a, int q, int j, int64_t& task, int& hh) {
-  const int64_t t0 = a.n_tasks * q / 8, t1 = a.n_tasks * (q + 1) / 8;
-  if (j >= 2 * (t1 - t0)) return false;
-  const int G = a.q_group;
-  if (G > 0) {
-    const int g = j / (2 * G), r = j - 2 * G * g;
-    const int64_t rest = t1 - t0 - (int64_t)g * G;
-    const int gs = rest < G ? (int)rest : G;
-    hh = r >= gs;
-    task = t0 + (int64_t)g * G + (r - hh * gs);
-  } else {
-    task = t0 + (j >> 1);
-    hh = j & 1;
-  }
-  return true;
-}
-
-// Layers 1 and 2 as ONE persistent queue (k_mpnn_x): a wave that finds layer 1's queues empty goes
-// on to layer 2's units instead of leaving, so layer 2 fills the wave slots layer 1's tail leaves
-// empty (and there is one launch ramp instead of two). A layer-2 unit of task t reads layer 1's
-// edge state and node features of t (and reuses t's agg rows) and the projection rows of its
-// senders' tasks, so it waits for layer 1's counter of t — which the node-update wave raises to 3
-// after its outputs are released — and, per edge block, for its senders' tasks; once layer 1's
-// finished-task count (q_head[120]) reads n_tasks, one acquire covers all of it and the waits stop.
-// No deadlock: a layer-2 wave waits only on layer-1 units already pulled by running waves, and
-// layer-1 units wait on nothing. W1 streams from L2 (KL = 0). Same operations per layer as
-// k_mpnn_q: identical bits.
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void k_mpnn_x(MpnnArgs a1_in, MpnnArgs a2_in) {
-  const MpnnArgsK a_k = (MpnnArgsK)__builtin_amdgcn_kernarg_segment_ptr();  // [0] layer 1, [1] layer 2
-  ClockStamp cs;
-  cs.start(a1_in.clk);
-  __shared__ float lds_scratch[NW][64 * 36];
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int q = __builtin_amdgcn_readfirstlane((int)(__builtin_amdgcn_s_getreg(0xf814) & 7));
-  int empty = 0, layer = 1;
-  bool l1_all_done = false;
-  for (;;) {
-    if (empty == 8) {
-      if (layer == 2) break;
-      layer = 2;
-      empty = 0;
-    }
-    MpnnArgsK ap = a_k + (layer - 1);
-    asm volatile("" : "+s"(ap));
-    const MpnnArgs& a = *(const MpnnArgs*)ap;
-    int j = 0;
-    if (lane == 0) j = __hip_atomic_fetch_add(a.q_head + 16 * q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    j = __builtin_amdgcn_readfirstlane(j);
-    int64_t task;
-    int hh;
-    if (!queue_unit(a, q, j, task, hh)) {
-      ++empty;
-      q = (q + 1) & 7;
-      continue;
-    }
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    if (layer == 1) {
-      mpnn_edge_blocks<1, 0, NW>(a, task, ln, 25 * hh, 25 * hh + 25, nullptr, lds_scratch, w);
-    } else {
-      const int32_t* dep = nullptr;
-      if (!l1_all_done) {
-        MpnnArgsK pp = a_k;
-        asm volatile("" : "+s"(pp));
-        const MpnnArgs& p = *(const MpnnArgs*)pp;
-        const int fin = __hip_atomic_load(p.q_head + 120, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (fin >= p.n_tasks) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          l1_all_done = true;
-        } else {
-          dep = p.q_done;
-          wait_tasks_done(dep, task);
-        }
-      }
-      mpnn_edge_blocks<2, 0, NW>(a, task, ln, 25 * hh, 25 * hh + 25, nullptr, lds_scratch, w, dep);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int prev = 0;
-    if (lane == 0) prev = __hip_atomic_fetch_add(a.q_done + task, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prev = __builtin_amdgcn_readfirstlane(prev);
-    if (prev == 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (layer == 1) {
-        mpnn_node_tile<1>(a, task * 32, ln, a.agg + task * 32 * 128);
-        // publish: h_out / P_out rows of this task, then its counter (-> 3) and the finished count
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-          __hip_atomic_fetch_add(a.q_done + task, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(a.q_head + 120, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else {
-        mpnn_node_tile<2>(a, task * 32, ln, a.agg + task * 32 * 128);
-      }
-    }
-  }
-  cs.stop(a_k->clk);
-}
-
-void launch_mpnn_x(const MpnnArgs& a1, const MpnnArgs& a2, hipStream_t st) {
-  const int64_t units = 2 * a1.n_tasks;
-  if (a1.q_waves == 8) {
-    const dim3 qgrid((unsigned)std::min<int64_t>((units + 7) / 8, a1.q_grid / 2));
-    hipLaunchKernelGGL(k_mpnn_x<8>, qgrid, dim3(512), 0, st, a1, a2);
-  } else {
-    const dim3 qgrid((unsigned)std::min<int64_t>((units + 3) / 4, a1.q_grid));
-    hipLaunchKernelGGL(k_mpnn_x<4>, qgrid, dim3(256), 0, st, a1, a2);
-  }
 }
 
 // Split layer (small batches, where one wave per 32 receivers cannot fill the GPU): the edge

@@ -40,7 +40,7 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free", "pst_write_files",
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
            "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_decode_ex", "pst_decoder_debug",
-           "pst_build_graph", "pst_clock_counters", "pst_pdb_batch_copy_f32")
+           "pst_build_graph", "pst_clock_counters", "pst_set_clock_counters", "pst_pdb_batch_copy_f32")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -89,6 +89,7 @@ def lib():
         L.pst_get_timing.argtypes = [P, P]
         L.pst_device_count.argtypes = [P]
         L.pst_clock_counters.argtypes = [P, P, ctypes.c_int32]
+        L.pst_set_clock_counters.argtypes = [P, ctypes.c_int32]
         L.pst_pdb_parse_files.argtypes = [P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_parse_strings.argtypes = [P, P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_batch_sizes.argtypes = [P, P, P]
@@ -312,6 +313,10 @@ class Tokenizer:
 
     def sync(self):
         self._check(lib().pst_sync(self._h))
+
+    def set_clock_counters(self, on: bool = True):
+        """Stamp the fused MPNN launches into the clock counters (off by default: measurement only)."""
+        self._check(lib().pst_set_clock_counters(self._h, 1 if on else 0))
 
     def clock_counters(self, reset: bool = False) -> np.ndarray:
         """Per fused MPNN layer since the last reset, uint64 [3, 8] (pst_clock_counters): shader

@@ -193,57 +193,6 @@ def test_token_ids_beyond_codebook_wrap_like_reference():
     assert np.array_equal(a, b)
 
 
-def test_fused_pair_kernel_matches_library_path(monkeypatch):
-    """k_pair_fused (one kernel over 32-pair tiles) against the library-GEMM pair path
-    (PST_DECODE_UNFUSED=1) on the same tokens: pair representation and atoms agree to float32
-    reordering noise, for a group of several proteins of different lengths."""
-    monkeypatch.setenv("PST_DEBUG", "1")
-    from pst_amd._native import Decoder
-    rng = np.random.default_rng(5)
-    toks = [rng.integers(0, 4096, n) for n in (37, 96, 5)]
-    dec = Decoder(0, 4096, 1, P.pack_decoder(P.random_full_params(6, 9), 6))
-    n_pairs = sum(len(t) ** 2 for t in toks)
-    fused = dec.decode(toks)
-    z_fused = dec.debug(1, n_pairs * 128).copy()
-    monkeypatch.setenv("PST_DECODE_UNFUSED", "1")
-    ref = dec.decode(toks)
-    z_ref = dec.debug(1, n_pairs * 128)
-    dec.close()
-    assert np.max(np.abs(z_fused - z_ref)) / np.max(np.abs(z_ref)) < 2e-5
-    for a, b in zip(fused, ref):
-        assert np.max(np.abs(a - b)) < 1e-3
-
-
-def test_fused_fold_tail_matches_separate_launches(monkeypatch):
-    """k_fold_tail (the structure module iteration's transition, affine update and sidechain
-    linears + both LayerNorms in one launch per 16-node tile, activations in LDS) against the 13
-    separate launches (PST_DECODE_UNFUSED_TAIL=1): a ragged group of proteins whose node counts are
-    not multiples of 16 (the partial last tile), df 1 and df 4; torsion angles, trajectory and atoms
-    agree to float32 reordering noise (one fma chain over k vs the split-K GEMMs)."""
-    monkeypatch.setenv("PST_DEBUG", "1")
-    from pst_amd._native import Decoder
-    rng = np.random.default_rng(23)
-    for cb, df, lens in ((4096, 1, (37, 96, 5, 131)), (64000, 4, (12, 33))):
-        D = len(LEVELS[cb])
-        toks = [rng.integers(0, cb, n) for n in lens]
-        dec = Decoder(0, cb, df, P.pack_decoder(P.random_full_params(D, 31), D))
-        n_nodes = df * sum(lens)
-        fused = dec.decode(toks)
-        traj_f = dec.debug(2, 8 * n_nodes * 7).copy()
-        ang_f = dec.debug(3, 8 * n_nodes * 6).copy()
-        monkeypatch.setenv("PST_DECODE_UNFUSED_TAIL", "1")
-        ref = dec.decode(toks)
-        traj_r = dec.debug(2, 8 * n_nodes * 7).copy()
-        ang_r = dec.debug(3, 8 * n_nodes * 6).copy()
-        monkeypatch.delenv("PST_DECODE_UNFUSED_TAIL")
-        dec.close()
-        assert np.all(np.isfinite(traj_f)) and np.all(np.isfinite(ang_f))
-        assert np.max(np.abs(ang_f - ang_r)) < 1e-4, (cb, df)
-        assert np.max(np.abs(traj_f - traj_r)) < 1e-3, (cb, df)
-        for a, b in zip(fused, ref):
-            assert np.max(np.abs(a - b)) < 1e-3
-
-
 def test_gemm_mfma_matches_valu_gemm(monkeypatch):
     """The per-node GEMMs run on the in-tree split-K f32-MFMA kernel (k_gemm_mfma, default) or on
     the LDS-tiled VALU kernel (PST_DECODE_NO_MFMA=1, one fma chain over k). The split K changes
@@ -261,27 +210,6 @@ def test_gemm_mfma_matches_valu_gemm(monkeypatch):
     for a, b in zip(base, other):
         assert np.all(np.isfinite(a)) and np.all(np.isfinite(b))
         assert np.max(np.abs(a - b)) < 1e-3
-
-
-def test_ipa_pair_sum_mfma_matches_valu_bitwise(monkeypatch):
-    """k_ipa_attn's pair attention Σ_j att[h][j]·z_ij on v_mfma_f32_16x16x4_f32 (default) vs the
-    VALU fmaf chains (PST_DECODE_IPA_VALU=1): the instruction is a k-ascending fmaf chain, so both
-    are the same in-order chain over j — identical bits, ragged group with key counts that are not
-    multiples of 4 (the zero-padded last k-step), df 1 and df 4."""
-    from pst_amd._native import Decoder
-    rng = np.random.default_rng(23)
-    for cb, df, lens in ((4096, 1, (64, 23, 130, 7)), (64000, 4, (9, 31, 128))):
-        D = len(LEVELS[cb])
-        toks = [rng.integers(0, cb, n) for n in lens]
-        dec = Decoder(0, cb, df, P.pack_decoder(P.random_full_params(D, 29), D))
-        base = dec.decode(toks)
-        monkeypatch.setenv("PST_DECODE_IPA_VALU", "1")
-        other = dec.decode(toks)
-        monkeypatch.delenv("PST_DECODE_IPA_VALU")
-        dec.close()
-        for a, b in zip(base, other):
-            assert np.all(np.isfinite(a))
-            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
 def test_decode_graph_replay_matches_direct_launches(monkeypatch):

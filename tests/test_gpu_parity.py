@@ -366,19 +366,17 @@ def test_mpnn_queue_identical_at_full_rounds(monkeypatch):
     # queue on every layer with the default unit order (groups of one XCD's wave slots), with
     # adjacent halves (group 0), and the default layers with a group size that leaves a partial
     # group in every XCD's range (3 072 / 8 = 384 tasks = 10 x 37 + 14)
-    # and layers 1-2 as one persistent launch (k_mpnn_x: cross-layer waits), 4- and 8-wave groups
-    for queue, layers, group, xl, qw in (("0", "-", "-", "0", "-"), ("1", "7", "-", "0", "-"),
-                                         ("1", "7", "0", "0", "-"), ("1", "-", "37", "0", "-"),
-                                         ("1", "-", "-", "1", "-"), ("1", "-", "-", "1", "4")):
+    # and the 4-wave queue workgroups
+    for queue, layers, group, qw in (("0", "-", "-", "-"), ("1", "7", "-", "-"), ("1", "7", "0", "-"),
+                                     ("1", "-", "37", "-"), ("1", "-", "-", "4")):
         monkeypatch.setenv("PST_MPNN_QUEUE", queue)
-        for k, v in (("PST_MPNN_QUEUE_LAYERS", layers), ("PST_MPNN_QGROUP", group), ("PST_MPNN_XLAYER", xl),
-                     ("PST_MPNN_QWAVES", qw)):
+        for k, v in (("PST_MPNN_QUEUE_LAYERS", layers), ("PST_MPNN_QGROUP", group), ("PST_MPNN_QWAVES", qw)):
             if v == "-":
                 monkeypatch.delenv(k, raising=False)
             else:
                 monkeypatch.setenv(k, v)
         tk = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
-        for rep in range(3 if (layers == "7" and group == "-") or xl == "1" else 1 if queue == "0" else 2):
+        for rep in range(3 if (layers == "7" and group == "-") else 1 if queue == "0" else 2):
             tok, nt, nn = tk.tokenize_packed(pos.astype(np.float32), flags, off)
             assert tk.last_plan_detail()["schedules"] == (["fused_queue"] if queue == "1" else ["fused"])
             hl = [tk.debug_fetch(w, R) for w in (1, 2, 3)]
@@ -396,9 +394,9 @@ def test_mpnn_queue_identical_at_full_rounds(monkeypatch):
 def test_mpnn_queue_forced_on_small_batches(lens, monkeypatch):
     """The persistent queue forced onto batches far below one round (4 to 20 tasks: most XCD
     ranges empty, a wave finds its own queue empty and steals from the others; the unit group larger
-    than a range) on every layer, with the default unit order and with adjacent halves, and the
-    cross-layer launch: node features after every layer and tokens equal the default schedule's
-    bit for bit."""
+    than a range) on every layer, with the default unit order, with adjacent halves and with 4-wave
+    workgroups: node features after every layer and tokens equal the default schedule's bit for
+    bit."""
     from pst_amd._native import Tokenizer, pack_samples
     samples = [synthetic.synthetic_protein(n, 5100 + i) for i, n in enumerate(lens)]
     pos, flags, off = pack_samples(samples)
@@ -409,11 +407,11 @@ def test_mpnn_queue_forced_on_small_batches(lens, monkeypatch):
     h0 = [ref.debug_fetch(w, R).view(np.uint32).copy() for w in (1, 2, 3)]
     ref.close()
     for env in ({"PST_MPNN_QUEUE_LAYERS": "7"}, {"PST_MPNN_QUEUE_LAYERS": "7", "PST_MPNN_QGROUP": "0"},
-                {"PST_MPNN_XLAYER": "1"}):
+                {"PST_MPNN_QUEUE_LAYERS": "7", "PST_MPNN_QWAVES": "4"}):
         monkeypatch.setenv("PST_SPLIT_TASKS", "0")
         monkeypatch.setenv("PST_HALF_TASKS", "0")
         monkeypatch.setenv("PST_MPNN_QUEUE", "1")
-        for k in ("PST_MPNN_QUEUE_LAYERS", "PST_MPNN_QGROUP", "PST_MPNN_XLAYER"):
+        for k in ("PST_MPNN_QUEUE_LAYERS", "PST_MPNN_QGROUP", "PST_MPNN_QWAVES"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)

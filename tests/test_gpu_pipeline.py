@@ -165,7 +165,8 @@ def test_two_proteins_small_first():
 
 
 def test_clock_counters_accumulate_and_reset():
-    """pst_clock_counters (bench.py's clock fields): each fused MPNN launch's stamping wave adds
+    """pst_clock_counters (bench.py's clock fields): off until pst_set_clock_counters enables them;
+    then each fused MPNN launch's stamping wave adds
     (shader cycles, 100 MHz ticks) and every wave its lifetime; two calls add about twice one call's
     ticks, reset restarts them, the implied clock is a plausible gfx950 shader clock, the queue
     form's wave-slot occupancy is high (one launch per layer: one chunk), and the tokens are
@@ -177,8 +178,11 @@ def test_clock_counters_accumulate_and_reset():
     t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
     tok0, _, _ = t.tokenize_packed(pos, flags, off)
     t.clock_counters(reset=True)
+    # off by default: a call stamps nothing until the counters are enabled
+    t.tokenize_packed(pos, flags, off)
     z = t.clock_counters()
     assert not z[:, [0, 1, 2, 4, 5]].any() and (z[:, 3] == np.iinfo(np.uint64).max).all()
+    t.set_clock_counters(True)
     tok1, _, _ = t.tokenize_packed(pos, flags, off)
     c1 = t.clock_counters().astype(np.float64)
     t.tokenize_packed(pos, flags, off)
