@@ -73,6 +73,7 @@ def main():
     ap.add_argument("--jobs", type=int, default=7)
     ap.add_argument("--stride", type=int, default=None)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--out", default=OUT, help="write here (a long run: merge into the fixture with compact_bench.py)")
     args = ap.parse_args()
     set_config(args.config)
     stride = args.stride or CONFIGS[args.config][5]
@@ -81,8 +82,10 @@ def main():
     if not _refenv.available():
         sys.exit("reference not available")
     sys.path.insert(0, _refenv.PKG)
-    old = dict(np.load(OUT)) if os.path.exists(OUT) else {}
-    todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old]
+    old = dict(np.load(args.out)) if os.path.exists(args.out) else {}
+    have = set(np.load(OUT).files) if os.path.exists(OUT) and args.out != OUT else set()
+    todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old
+            and f"{case_name(p)}/tokens" not in have and f"{case_name(p)}/tokens_pe32" not in have]
     print(f"{len(todo)} proteins to run", flush=True)
     done = 0
     with get_context("spawn").Pool(args.jobs) as pool:
@@ -93,9 +96,9 @@ def main():
             print(f"p{p}: T={res['meta'][1]} min margin={res['margin_pe32'].min():.3e} ({dt:.0f} s) "
                   f"[{done}/{len(todo)}]", flush=True)
             if done % 16 == 0:  # checkpoint: a killed run resumes where it stopped
-                np.savez_compressed(OUT, **old)
-    np.savez_compressed(OUT, **old)
-    print("wrote", OUT)
+                np.savez_compressed(args.out, **old)
+    np.savez_compressed(args.out, **old)
+    print("wrote", args.out)
 
 
 if __name__ == "__main__":
