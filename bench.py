@@ -197,79 +197,50 @@ def plan_only(args, rank, world):
 
 
 def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
-    """Token ids of the fixture proteins this rank holds vs the reference's own forward
-    (Vq3D.encode_and_quantize under the shim, float64 with JAX's float32 PE argument, i.e. the
-    reference's PE values): every 4th protein of the headline workload
-    (forward_ref_bench.npz, 256 proteins, make_forward_bench.py; config 5's workload: every 16th,
-    32 proteins), plus the proteins of
-    forward_ref_wide.npz the workload holds (bench256 p0-7, 200, 511, 777, 1023; bench512 p0-1 at
-    64000/df 4). With `bounded` (our FSQ-bounded latents, pst_aux) the report carries our
-    deviation from the reference's latent and its ratio to the rounding margin (refwide.report)."""
+    """Token ids of this rank's proteins vs the reference's own forward (Vq3D.encode_and_quantize
+    under the shim, float64 with JAX's float32 PE argument, i.e. the reference's PE values):
+    tests/golden/forward_ref_bench.npz holds EVERY protein of the headline workload (bench256:
+    1 024 proteins, 262 144 tokens) and every 16th of config 5's (bench512), with per-token margins
+    and the bounded latents of the close tokens (refwide.BenchSample). Every mismatch is listed with
+    its protein, token, latent dim, the reference's margin and our deviation; with `bounded` (our
+    FSQ-bounded latents, pst_aux) the report carries our deviation on every close token."""
     try:
         import refwide
-        F = refwide.load()
     except Exception:
         return None
-    # the bench fixture's sample of this workload: config 3 (bench256_*, every 4th protein) or
-    # config 5 (bench512_*, every 16th)
-    bkey = {(4096, 1, 256): "bench256_p{}", (64000, 4, 512): "bench512_p{}"}.get((args.codebook, args.df, args.residues))
+    name = {(4096, 1, 256): "bench256", (64000, 4, 512): "bench512"}.get((args.codebook, args.df, args.residues))
+    if name is None:
+        return None
     try:
-        FB = refwide.load_bench() if bkey else None
+        S = refwide.load_bench_sample(name)
     except Exception:
-        FB = None
-    tag = {(4096, 1, 256): "bench256_p{}_k4096_df1", (64000, 4, 512): "bench512_p{}_k64000_df4"}.get(
-        (args.codebook, args.df, args.residues))
-    if tag is None:
         return None
-    reps, prots, src = [], [], {}
-    for i, p in enumerate(ids):
-        if FB is not None and bkey.format(p) + "/tokens_pe32" in FB.files:
-            c, G, want = bkey.format(p), FB, None
-        elif tag.format(p) + "/tokens" in F.files:
-            c, G = tag.format(p), F
-            want = F[c + "/tokens"]
-        else:
-            continue
-        T = int(G[c + "/meta"][1])
-        got = tok[off[i]:off[i] + T]
-        bref = G[c + "/bounded_pe32"] if c + "/bounded_pe32" in G.files else G[c + "/bounded"]
-        tref = G[c + "/tokens_pe32"] if c + "/tokens_pe32" in G.files else want
-        bours = bounded[off[i]:off[i] + T] if bounded is not None else bref  # no deviation known: margins only
-        r = refwide.report(bref, tref, bours, got)
-        if want is not None:
-            r["identical_to_f64_reference"] = int(np.sum(got == want))
-        reps.append(r)
-        prots.append(p)
-        src[p] = "forward_ref_bench" if G is FB else "forward_ref_wide"
-    if not reps:
+    pos_of = {p: i for i, p in enumerate(ids)}
+    prots = [p for p in ids if p in S.index]
+    if not prots:
         return None
-    r = refwide.merge(reps)
+    sl = [slice(int(off[pos_of[p]]), int(off[pos_of[p]]) + S.n_tokens(p)) for p in prots]
+    r = S.compare(prots, [tok[x] for x in sl], [bounded[x] for x in sl] if bounded is not None else None)
     cuts = plan["cuts"] if plan else None
-    chunk_of = {}
-    if cuts:
-        pos_of = {p: i for i, p in enumerate(ids)}
-        chunk_of = {p: int(np.searchsorted(cuts, pos_of[p], side="right") - 1) for p in prots}
     by_chunk = {}
-    for p, rep in zip(prots, reps):
-        k = str(chunk_of.get(p, 0))
+    for p, x in zip(prots, sl):
+        k = str(int(np.searchsorted(cuts, pos_of[p], side="right") - 1)) if cuts else "0"
         b = by_chunk.setdefault(k, {"proteins": 0, "tokens": 0, "identical": 0})
         b["proteins"] += 1
-        b["tokens"] += rep["tokens"]
-        b["identical"] += rep["identical"]
-    return {"proteins_compared": len(prots), "proteins_from_bench_fixture": sum(v == "forward_ref_bench" for v in src.values()),
-            "tokens_compared": r["tokens"], "identical": r["identical"], "rate": r["rate"],
-            "by_pipeline_chunk": by_chunk,
-            "identical_to_f64_reference": int(sum(x.get("identical_to_f64_reference", 0) for x in reps)),
-            "f64_reference_tokens_compared": int(sum(x["tokens"] for x in reps if "identical_to_f64_reference" in x)),
-            "min_margin": r["min_margin"],
-            "max_deviation": r["max_deviation"] if bounded is not None else None,
-            "max_deviation_over_margin": r["max_deviation_over_margin"] if bounded is not None else None,
-            "mismatches_explained_by_rounding": r["mismatches_explained_by_rounding"],
+        b["tokens"] += x.stop - x.start
+        b["identical"] += int(np.sum(tok[x] == S.ref_tokens(p)))
+    return {"proteins_compared": r["proteins"], "proteins_in_workload": len(ids), "tokens_compared": r["tokens"],
+            "identical": r["identical"], "rate": r["rate"], "by_pipeline_chunk": by_chunk,
+            "min_margin": r["min_margin"], "close_tokens": r["close_tokens"], "close_below": r["close_below"],
+            "max_deviation_close": r["max_deviation_close"],
+            "max_deviation_over_margin_close": r["max_deviation_over_margin_close"],
+            "mismatches": r["mismatches"], "mismatches_explained_by_rounding": r["mismatches_explained_by_rounding"],
+            "unlisted_mismatches": len(r["unlisted"]), "known_cases_not_flipped": r["missing_known"],
             "margin_histogram_all": r["margin_histogram_all"],
             "margin_histogram_mismatches": r["margin_histogram_mismatches"],
             "against": "reference Vq3D.encode_and_quantize run in float64 under the shim with JAX's float32 "
-                       "PE argument (tests/golden/forward_ref_bench.npz: every 4th protein of the workload, "
-                       "make_forward_bench.py; tests/golden/forward_ref_wide.npz, make_forward_wide.py)"}
+                       f"PE argument (tests/golden/forward_ref_bench.npz '{name}': {len(S)} proteins of the workload, "
+                       "make_forward_bench.py + compact_bench.py)"}
 
 
 def clock_stats(per_step, steps=None):
@@ -374,7 +345,17 @@ def _ref_as_computed_rate(model, pf, df, threads, cores, what):
                       f"the C graph, one protein per call; torch.set_num_threads({threads}) of {cores} cores available"}, toks
 
 
-def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=None, casp=None):
+def _reference_sample(args):
+    """refwide.BenchSample of this workload (None when there is none)."""
+    name = {(4096, 1, 256): "bench256", (64000, 4, 512): "bench512"}.get((args.codebook, args.df, args.residues))
+    try:
+        import refwide
+        return refwide.load_bench_sample(name) if name else None
+    except Exception:
+        return None
+
+
+def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=None, casp=None, ref_ids=None):
     """CPU baselines (reported, not targeted): the reference-as-computed PyTorch-CPU
     forward on a `--cpu-sample`-protein subset of the workload (every 16th protein by default, so
     both pipeline chunks) and on SURVEY config 2 (the 31 CASP14 structures, `casp` = (positions,
@@ -391,16 +372,26 @@ def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=No
     csel = np.arange(0, nb, max(1, nb // max(1, n)))[:n]
     pf = [(samples[i].atom37_positions, samples[i].atom_flags()) for i in csel]
     out = {}
-    ident = None
     for threads in sorted({cores, 8}, reverse=True):
         log(f"reference-as-computed CPU baseline (config 3 subset), {threads} threads, {len(pf)} proteins")
         out[threads], toks = _ref_as_computed_rate(model, pf, args.df, threads, cores,
                                                    f"every {max(1, nb // max(1, n))}th protein of the workload")
-        if ident is None:
-            # protein i's T = n_i / df tokens sit at gpu_tok[off[i] .. off[i] + T) (raw-offset layout)
-            ms = [min(len(t), int(off[i + 1] - off[i]) // args.df) for t, i in zip(toks, csel)]
-            ident = sum(int(np.sum(t[:m] == gpu_tok[off[i]:off[i] + m])) for t, i, m in zip(toks, csel, ms))
-            out[threads]["tokens_identical_to_gpu"] = f"{ident} / {sum(ms)}"
+        # protein i's T = n_i / df tokens sit at gpu_tok[off[i] .. off[i] + T) (raw-offset layout)
+        ms = [min(len(t), int(off[i + 1] - off[i]) // args.df) for t, i in zip(toks, csel)]
+        ident = sum(int(np.sum(t[:m] == gpu_tok[off[i]:off[i] + m])) for t, i, m in zip(toks, csel, ms))
+        out[threads]["tokens_identical_to_gpu"] = f"{ident} / {sum(ms)}"
+        # against the reference itself: PyTorch-CPU float32 reduces in a thread-count-dependent
+        # order, so a token whose reference margin is below its deviation may flip in one setting
+        # and not another; every difference is listed with its reference margin
+        ref = _reference_sample(args)
+        if ref is not None:
+            ids_s = [ref_ids[i] for i in csel] if ref_ids is not None else list(csel)
+            keep = [k for k, p in enumerate(ids_s) if p in ref.index]
+            rr = ref.compare([ids_s[k] for k in keep], [toks[k][:ref.n_tokens(ids_s[k])] for k in keep])
+            out[threads]["tokens_identical_to_reference"] = f"{rr['identical']} / {rr['tokens']}"
+            out[threads]["mismatches_vs_reference"] = [
+                {k: m[k] for k in ("protein", "token", "ref_margin", "dim") if k in m} for m in rr["mismatches"]]
+            out[threads]["unexplained_vs_reference"] = len(rr["unexplained"])
     cfg2 = {}
     if casp is not None and args.codebook == 4096 and args.df == 1:
         cpos, cflags, coff, ctok = casp
@@ -640,7 +631,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baselines")
         cpu, cpu8, cpu_c2, cpu_c2_8, port, exact = cpu_baselines(args, samples, blob, levels, pos, flags, off, tok,
-                                                                 plan, casp)
+                                                                 plan, casp, ref_ids=ids)
 
     if rank == 0:
         mode = "weak" if args.weak else "strong"

@@ -1,24 +1,29 @@
-"""Reference-forward fixture for the HEADLINE workload's exact-match sample (build container only).
+"""Reference-forward fixture for the HEADLINE workload (build container only).
 
-`bench.py` checks token ids against the oracle on every 8th protein of
-`synthetic_batch(1024, 256, seed=1000)`; this fixture pins every 4th (proteins 0, 4, …, 1020: 256
-proteins, 65 536 tokens, both pipeline chunks) to the reference. This script runs the
-REFERENCE's own `Vq3D.encode_and_quantize` (model.py:453-479) under the import shim on each of
-them — the `_pe32` rendering of `make_forward_wide.py` (float64 with the sinusoidal PE argument
-rounded to float32 exactly as JAX forms it with x64 off, i.e. the reference's own PE values) —
-at codebook 4096, df 1, random weights `params.random_params(6, 1234)` (the bench's).
+This script runs the REFERENCE's own `Vq3D.encode_and_quantize` (model.py:453-479) under the
+import shim on proteins of bench.py's workload — the `_pe32` rendering of `make_forward_wide.py`
+(float64 with the sinusoidal PE argument rounded to float32 exactly as JAX forms it with x64 off,
+i.e. the reference's own PE values) — at codebook 4096, df 1, random weights
+`params.random_params(6, 1234)` (the bench's). Round 4 ran every 4th protein of
+`synthetic_batch(1024, 256, seed=1000)` (`--stride 4`, 256 proteins); round 5 ran the other 768
+(`--stride 1`, ~80 s per protein on one core, ~2.8 h on 6 workers), so every protein of the
+headline workload is pinned.
 
 `--config 5` does the same for SURVEY config 5's workload (`bench.py --codebook 64000 --df 4
 --residues 512 --proteins 512`: synthetic_batch(512, 512, seed=1000)), every 16th protein (32
-proteins, 4 096 tokens), case names `bench512_p{p}`, in the same file.
+proteins, 4 096 tokens), case names `bench512_p{p}`.
 
-Kept per protein `bench256_p{p}`: the reference's token ids, its FSQ-bounded latents (float64),
-the per-token rounding margin, `meta` = [n, T, codebook, df, D, seed], and the SHA-256 of the
-float32 inputs plus the generator arguments. The inputs themselves are NOT stored: they are
-regenerated from `pst_amd.synthetic.synthetic_protein(256, 1000 + p)` and must hash to the stored
-SHA (`tests/test_fixture_recipes.py`), which keeps the file small and the recipe honest.
+Raw output per protein `bench{n_res}_p{p}` (into `--out`, a scratch file outside the fixture):
+the reference's token ids, its FSQ-bounded latents (float64), the per-token rounding margin,
+`meta` = [n, T, codebook, df, D, seed], the SHA-256 of the float32 inputs and the generator
+arguments. `compact_bench.py RAW…` packs them into the committed `forward_ref_bench.npz` (tokens,
+margins, and the latents of the tokens within refwide.CLOSE of a boundary). Proteins already in
+the committed fixture are skipped. The inputs themselves are not stored: they are regenerated
+from `pst_amd.synthetic.synthetic_protein(n_res, 1000 + p)` and must hash to the stored SHA
+(`tests/test_fixture_recipes.py`).
 
-    python tests/golden/make_forward_bench.py [--jobs 7] [--stride 4] [--config 3|5]
+    python tests/golden/make_forward_bench.py --out RAW.npz [--jobs 6] [--stride 1] [--config 3|5]
+    python tests/golden/compact_bench.py RAW.npz [RAW2.npz …]
 """
 import argparse
 import os
@@ -40,7 +45,7 @@ def set_config(cfg):
     N_PROT, N_RES, SEED0, CODEBOOK, DF, _ = CONFIGS[cfg]
 
 
-def proteins(stride=8):
+def proteins(stride=4):
     return list(range(0, N_PROT, stride))
 
 
@@ -73,7 +78,7 @@ def main():
     ap.add_argument("--jobs", type=int, default=7)
     ap.add_argument("--stride", type=int, default=None)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
-    ap.add_argument("--out", default=OUT, help="write here (a long run: merge into the fixture with compact_bench.py)")
+    ap.add_argument("--out", required=True, help="raw per-protein output (merged into the fixture by compact_bench.py)")
     args = ap.parse_args()
     set_config(args.config)
     stride = args.stride or CONFIGS[args.config][5]
@@ -83,9 +88,12 @@ def main():
         sys.exit("reference not available")
     sys.path.insert(0, _refenv.PKG)
     old = dict(np.load(args.out)) if os.path.exists(args.out) else {}
-    have = set(np.load(OUT).files) if os.path.exists(OUT) and args.out != OUT else set()
-    todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old
-            and f"{case_name(p)}/tokens" not in have and f"{case_name(p)}/tokens_pe32" not in have]
+    import refwide
+    name = case_name(0).split("_p")[0]
+    have = set()
+    if os.path.exists(OUT) and f"{name}/proteins" in np.load(OUT).files:
+        have = {int(p) for p in refwide.load_bench_sample(name).proteins}
+    todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old and p not in have]
     print(f"{len(todo)} proteins to run", flush=True)
     done = 0
     with get_context("spawn").Pool(args.jobs) as pool:

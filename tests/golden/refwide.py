@@ -14,8 +14,16 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PATH = os.path.join(HERE, "forward_ref_wide.npz")
-# the headline workload's exact-match sample (every 8th bench protein, make_forward_bench.py)
+# the headline workload pinned to the reference (make_forward_bench.py + compact_bench.py): every
+# protein of bench.py's config-3 workload (bench256) and every 16th of config 5's (bench512)
 BENCH_PATH = os.path.join(HERE, "forward_ref_bench.npz")
+# tokens whose reference margin is below CLOSE keep their bounded latent in the compact fixture
+CLOSE = 1e-4
+# The headline workload's tokens that a float32 implementation resolves to the other side of a
+# rounding boundary than the reference's float64 evaluation: (sample, protein, token) -> the latent
+# dim whose margin our deviation exceeds. Every other token must be identical; an unlisted flip, or
+# a listed one that no longer flips, fails the tests.
+KNOWN_BOUNDARY_CASES = {("bench256", 924, 3): 5}
 # log10 bins of the margin histogram: [0, 1e-7), [1e-7, 1e-6), ..., [1e-1, 0.5]
 EDGES = [0.0, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2, 1e-1, 0.5000001]
 
@@ -113,3 +121,110 @@ def device_outputs(F, make_tokenizer, prefix=""):
             a = int(off[i])
             out[c] = (tok[a:a + T].copy(), aux["bounded"][a:a + T].copy(), aux["pre_proj"][a:a + T].copy())
     return out
+
+
+class BenchSample:
+    """One workload of the compact `forward_ref_bench.npz` (`compact_bench.py`): the reference's
+    token ids and per-token rounding margins of every listed protein, and its bounded latents of
+    the tokens whose margin is below CLOSE (the only ones a float32 implementation can flip).
+    Inputs are not stored: protein p is synthetic_protein(n_res, seed0 + p) and must hash to
+    input_sha256 (tests/test_fixture_recipes.py)."""
+
+    def __init__(self, F, name):
+        g = lambda k: F[f"{name}/{k}"]
+        self.name = name
+        self.proteins = g("proteins").astype(np.int64)
+        self.tok_off = g("tok_off").astype(np.int64)
+        self.tokens = g("tokens").astype(np.uint32)
+        self.margin = g("margin").astype(np.float64)
+        self.n_nodes = g("n_nodes").astype(np.int64)
+        self.close = g("close").astype(np.int64)
+        self.close_bounded = g("close_bounded").astype(np.float64)
+        self.input_sha256 = g("input_sha256")
+        n_res, seed0, cb, df, D, pseed = (int(v) for v in g("meta"))
+        self.meta = {"n_res": n_res, "seed0": seed0, "codebook": cb, "df": df, "D": D, "param_seed": pseed}
+        self.index = {int(p): i for i, p in enumerate(self.proteins)}
+
+    def __len__(self):
+        return len(self.proteins)
+
+    def ref_tokens(self, p):
+        i = self.index[int(p)]
+        return self.tokens[self.tok_off[i]:self.tok_off[i + 1]]
+
+    def n_tokens(self, p):
+        i = self.index[int(p)]
+        return int(self.tok_off[i + 1] - self.tok_off[i])
+
+    def compare(self, prots, ours, bounded=None):
+        """Exact match of `ours` (token ids per protein of `prots`) against the reference; with
+        `bounded` (our FSQ-bounded latents per protein) the deviation |b_ours - b_ref| on every
+        close token. Each mismatch is listed with its reference margin, the dim whose rounding
+        differs and our deviation there; `unexplained` lists mismatches whose margin is not below
+        CLOSE or not below our deviation (a real error, never rounding), `unlisted` the ones missing
+        from KNOWN_BOUNDARY_CASES, `missing_known` the listed cases of these proteins that did not
+        flip."""
+        close_pos = {int(f): j for j, f in enumerate(self.close)}
+        n_tok = n_eq = n_close = 0
+        mism, unexplained, unlisted = [], [], []
+        dev_close, ratio_close = [], []
+        mm_all, mm_bad = [], []
+        for k, p in enumerate(prots):
+            i = self.index[int(p)]
+            a, b = int(self.tok_off[i]), int(self.tok_off[i + 1])
+            ref = self.tokens[a:b]
+            got = np.asarray(ours[k])[:b - a].astype(np.uint32)
+            if len(got) != b - a:
+                raise AssertionError(f"{self.name} p{p}: {len(got)} tokens vs reference {b - a}")
+            n_tok += b - a
+            bad = np.nonzero(got != ref)[0]
+            n_eq += (b - a) - len(bad)
+            mm_all.append(self.margin[a:b])
+            mm_bad.append(self.margin[a + bad])
+            bo = None if bounded is None else np.asarray(bounded[k], np.float64)[:b - a]
+            # close tokens of this protein: our deviation against the reference's margin per dim
+            cl = [(int(f), close_pos[int(f)]) for f in self.close[(self.close >= a) & (self.close < b)]]
+            n_close += len(cl)
+            if bo is not None:
+                for f, j in cl:
+                    bref = self.close_bounded[j]
+                    dm = dim_margins(bref)
+                    dv = np.abs(bo[f - a, :len(bref)] - bref)
+                    dev_close.append(float(dv.max()))
+                    ratio_close.append(float((dv / np.maximum(dm, 1e-300)).max()))
+            for t in bad:
+                f = a + int(t)
+                rec = {"protein": int(p), "token": int(t), "ref_token": int(ref[t]), "our_token": int(got[t]),
+                       "ref_margin": float(self.margin[f])}
+                if f in close_pos:
+                    bref = self.close_bounded[close_pos[f]]
+                    dm = dim_margins(bref)
+                    d = int(np.argmin(dm))
+                    rec["dim"] = d
+                    rec["ref_latent"] = float(bref[d])
+                    if bo is not None:
+                        rec["our_latent"] = float(bo[t, d])
+                        rec["our_deviation"] = float(abs(bo[t, d] - bref[d]))
+                ok = f in close_pos and ("our_deviation" not in rec or rec["our_deviation"] > rec["ref_margin"])
+                (mism if ok else unexplained).append(rec)
+                if KNOWN_BOUNDARY_CASES.get((self.name, int(p), int(t))) != rec.get("dim"):
+                    unlisted.append(rec)
+        held = {int(p) for p in prots}
+        flipped = {(r["protein"], r["token"]) for r in mism + unexplained}
+        missing = [list(k) for k in KNOWN_BOUNDARY_CASES
+                   if k[0] == self.name and k[1] in held and (k[1], k[2]) not in flipped]
+        mall = np.concatenate(mm_all) if mm_all else np.zeros(0)
+        mbad = np.concatenate(mm_bad) if mm_bad else np.zeros(0)
+        return {"proteins": len(prots), "tokens": n_tok, "identical": n_eq, "rate": n_eq / max(1, n_tok),
+                "min_margin": float(mall.min()) if len(mall) else None,
+                "close_tokens": n_close, "close_below": CLOSE,
+                "max_deviation_close": max(dev_close) if dev_close else None,
+                "max_deviation_over_margin_close": max(ratio_close) if ratio_close else None,
+                "margin_histogram_all": histogram(mall), "margin_histogram_mismatches": histogram(mbad),
+                "mismatches": mism + unexplained, "unexplained": unexplained, "unlisted": unlisted,
+                "missing_known": missing,
+                "mismatches_explained_by_rounding": not unexplained}
+
+
+def load_bench_sample(name="bench256", F=None):
+    return BenchSample(F if F is not None else load_bench(), name)

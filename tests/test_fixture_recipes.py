@@ -42,15 +42,19 @@ def test_casp14_inputs_match_atom37_fixture():
 
 
 def test_bench_fixture_inputs_reproduce():
-    """forward_ref_bench.npz stores no inputs: every 4th protein of bench.py's workload (and every
-    16th of config 5's) must regenerate to the SHA-256 the reference forward ran on."""
-    FB = refwide.load_bench()
-    assert refwide.cases(FB, "bench256_") == sorted(f"bench256_p{p}" for p in range(0, 1024, 4))
-    # config 5's sample (make_forward_bench.py --config 5): every 16th of 512 x 512 residues
-    assert refwide.cases(FB, "bench512_") == sorted(f"bench512_p{p}" for p in range(0, 512, 16))
-    names = refwide.cases(FB)
-    for c in names:
-        n_res, seed = (int(v) for v in FB[c + "/synthetic_args"])
-        assert (n_res, seed) == (int(c[5:8]), 1000 + int(c.split("_p")[1]))
-        s = synthetic.synthetic_protein(n_res, seed)
-        assert M.input_sha(s.atom37_positions.astype(np.float32), s.atom_flags()) == str(FB[c + "/input_sha256"]), c
+    """forward_ref_bench.npz stores no inputs: every protein of bench.py's headline workload (and
+    every 16th of config 5's) must regenerate to the SHA-256 the reference forward ran on."""
+    for name, n_res, want in (("bench256", 256, None), ("bench512", 512, list(range(0, 512, 16)))):
+        S = refwide.load_bench_sample(name)
+        prots = [int(p) for p in S.proteins]
+        if want is not None:
+            assert prots == want
+        else:
+            assert prots == sorted(prots) and set(range(0, 1024, 4)) <= set(prots)
+        assert S.meta["n_res"] == n_res and S.meta["seed0"] == 1000
+        assert len(S.tok_off) == len(prots) + 1 and S.tok_off[-1] == len(S.tokens) == len(S.margin)
+        assert (S.margin[S.close] < refwide.CLOSE).all() and (np.delete(S.margin, S.close) >= refwide.CLOSE).all()
+        assert np.array_equal(refwide.dim_margins(S.close_bounded).min(-1).astype(np.float32), S.margin[S.close])
+        for i, p in enumerate(prots):
+            s = synthetic.synthetic_protein(n_res, 1000 + p)
+            assert M.input_sha(s.atom37_positions.astype(np.float32), s.atom_flags()) == str(S.input_sha256[i]), p
