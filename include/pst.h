@@ -217,6 +217,14 @@ int pst_decoder_decode_ex(pst_decoder* dec, const uint32_t* tokens, const int64_
  * [per protein 8, N, 3, 2], 4 atom14 [sum N, 14, 3]. */
 int pst_decoder_debug(pst_decoder* dec, int32_t which, float* out, size_t n_floats);
 
+/* Decoder stage timing (measurement; tools/bench_decode.py's roofline): while enabled, every
+ * group is launched directly (no graph replay) with HIP events around its stages, and
+ * pst_decoder_get_timing returns ms[0..3] summed over the groups since enabling: upsampler,
+ * pair-chain inputs (LayerNorm + left/right/init GEMMs), k_pair_fused, the 8 fold iterations. */
+#define PST_DECODER_N_STAGES 4
+int pst_decoder_set_timing(pst_decoder* dec, int32_t enable);
+int pst_decoder_get_timing(pst_decoder* dec, float* ms);
+
 /*
  * Native PDB parsing (host, no GPU): replaces protein_structure_from_pdb_string
  * (structure_tokenizer/data/protein_structure_sample.py:166-248, Biopython PDBParser semantics,

@@ -343,12 +343,20 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   for (int l = 0; l < 3; ++l) {
     const Layer& S = P.L[l];
     LayerOff& O = ctx->L[l];
+    // The GEMMs that consume a GELU output (MLP layers 1 and 2 — for the message MLP, layer 2
+    // runs on the segment sums of GELU outputs — and the FFN's second layer) get their weights
+    // scaled by 0.5: the kernels evaluate 2·GELU in one fma less (c_gelu2x, pst_device.h), and
+    // (2g)·(w/2) = g·w exactly, so every chain is the canonical one the oracle computes
+    auto half = [](std::vector<float> v) {
+      for (float& x : v) x *= 0.5f;
+      return v;
+    };
     auto mlp = [&](const Lin* m, MlpOff& o) {
       o.w0 = A.add(frag(m[0].w, H, 256, 128, 128, 0, 128));
       o.b0 = A.add(perm(m[0].b));
-      o.w1 = A.add(frag(m[1].w, H, 0, 128, 128, 0, 128));
+      o.w1 = A.add(half(frag(m[1].w, H, 0, 128, 128, 0, 128)));
       o.b1 = A.add(perm(m[1].b));
-      o.w2 = A.add(frag(m[2].w, H, 0, 128, 128, 0, 128));
+      o.w2 = A.add(half(frag(m[2].w, H, 0, 128, 128, 0, 128)));
       o.b2 = A.add(perm(m[2].b));
       o.bf0 = A.add(bfrag(m[0].b));
       o.bf1 = A.add(bfrag(m[1].b));
@@ -364,7 +372,7 @@ int build_weights(pst_ctx* ctx, const float* blob) {
       w1.insert(w1.end(), f.begin(), f.end());
       auto bp = perm(S.ff[0].b + 128 * ck);
       b1.insert(b1.end(), bp.begin(), bp.end());
-      auto g = frag(S.ff[1].w, H, 128 * ck, 128, 128, 0, 128);
+      auto g = half(frag(S.ff[1].w, H, 128 * ck, 128, 128, 0, 128));
       w2.insert(w2.end(), g.begin(), g.end());
     }
     O.ff_w1 = A.add(w1);

@@ -936,6 +936,12 @@ struct pst_decoder {
   hipEvent_t up_ev = nullptr;
   // decode_group's kernel sequence as HIP graphs, keyed by the group's shape (decode_group)
   std::map<std::vector<int64_t>, hipGraphExec_t> graphs;
+  // stage timing (pst_decoder_set_timing; measurement): HIP events around the upsampler, the pair
+  // chain's inputs, k_pair_fused and the 8 fold iterations, launched directly (no graph replay)
+  // while enabled; ms summed over the groups of the calls since enabling
+  bool timing = false;
+  hipEvent_t tev[PST_DECODER_N_STAGES + 1] = {};
+  float tms[PST_DECODER_N_STAGES] = {};
 };
 
 namespace {
@@ -1538,7 +1544,11 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   }
   DecBatch bt{G.B, S.tok_off, S.node_off, S.pair_off, S.tok_prot, S.node_prot};
   const int Ni = (int)N;
+  auto mark = [&](int i) {
+    if (dec->timing) (void)hipEventRecord(dec->tev[i], st);
+  };
   auto launch = [&]() -> int {
+    mark(0);
     // ---- upsampler (CrossAttentionScaler, use_original_posenc)
     hipLaunchKernelGGL(k_up_init, dim3((unsigned)T), dim3(128), 0, st, S.tokens, bt, T, dec->d_levels, dec->D,
                        W.up_proj.w, W.up_proj.b, dec->d_pe_tok, S.orig_in);
@@ -1561,6 +1571,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
       hipLaunchKernelGGL(k_transition128, dim3((unsigned)((T + FT_NODES - 1) / FT_NODES)), dim3(512), 0, st, tb);
     }
     hipLaunchKernelGGL(k_spherical, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.res, Ni);  // s_i
+    mark(1);
     // ---- sequence decoder: pair representation over each protein's N_b² pairs
     layernorm(st, S.res, 128, S.ln_a, 128, Ni, 128, W.pr_ln_in);
     gemm(st, S.ln_a, 128, W.left, S.left, 256, Ni, 0);
@@ -1576,7 +1587,9 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
     pa.NP = NP;
     pa.bt = bt;
     const int64_t tiles = (NP + 31) / 32;
+    mark(2);
     hipLaunchKernelGGL(k_pair_fused, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, pa);
+    mark(3);
     hipLaunchKernelGGL(k_affine_init, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, Ni);
     // relu(init_act) feeds the angle resnet of every iteration: once, not 8 copies
     hipLaunchKernelGGL(k_relu_copy, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, S.init_act, 128, S.init_relu,
@@ -1605,7 +1618,7 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
                          S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7, last ? S.atom37 : nullptr,
                          last ? S.atom14 : nullptr, Ni);
     }
-
+    mark(4);
     DCHK(hipGetLastError());
     return PST_OK;
   };
@@ -1613,10 +1626,18 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
   // replayed (the decode was partly launch-bound: kernel time 5.0 ms of ~5.7 ms per 8 x 256
   // decode). Inputs are uploaded above, outside the graph; every kernel argument is a function of
   // the shape (per-protein token / node counts) and the decoder's fixed buffers.
-  const bool use_graph = !keep_debug && !getenv("PST_DECODE_NO_GRAPH");
+  const bool use_graph = !keep_debug && !dec->timing && !getenv("PST_DECODE_NO_GRAPH");
   if (!use_graph) {
     int rc = launch();
     if (rc) return rc;
+    if (dec->timing) {
+      DCHK(hipEventSynchronize(dec->tev[PST_DECODER_N_STAGES]));
+      for (int i = 0; i < PST_DECODER_N_STAGES; ++i) {
+        float ms = 0.0f;
+        DCHK(hipEventElapsedTime(&ms, dec->tev[i], dec->tev[i + 1]));
+        dec->tms[i] += ms;
+      }
+    }
   } else {
     std::vector<int64_t> key{(int64_t)t_mfma, G.B};
     key.insert(key.end(), G.node_off.begin(), G.node_off.end());
@@ -1678,6 +1699,22 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
 }  // namespace
 
 extern "C" {
+
+int pst_decoder_set_timing(pst_decoder* dec, int32_t enable) {
+  if (!dec) return PST_E_INVALID;
+  DCHK(hipSetDevice(dec->device));
+  if (enable && !dec->tev[0])
+    for (int i = 0; i <= PST_DECODER_N_STAGES; ++i) DCHK(hipEventCreate(&dec->tev[i]));
+  dec->timing = enable != 0;
+  for (float& v : dec->tms) v = 0.0f;
+  return PST_OK;
+}
+
+int pst_decoder_get_timing(pst_decoder* dec, float* ms) {
+  if (!dec || !ms) return PST_E_INVALID;
+  for (int i = 0; i < PST_DECODER_N_STAGES; ++i) ms[i] = dec->tms[i];
+  return PST_OK;
+}
 
 size_t pst_decoder_param_count(int32_t n_levels) {
   DecWeights W;
@@ -1854,6 +1891,8 @@ int pst_decoder_destroy(pst_decoder* dec) {
   if (dec->h_up) (void)hipHostFree(dec->h_up);
   if (dec->h_atoms) (void)hipHostFree(dec->h_atoms);
   if (dec->up_ev) (void)hipEventDestroy(dec->up_ev);
+  for (auto& e : dec->tev)
+    if (e) (void)hipEventDestroy(e);
   if (dec->stream) (void)hipStreamDestroy(dec->stream);
   delete dec;
   return PST_OK;

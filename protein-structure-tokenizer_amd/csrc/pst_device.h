@@ -80,9 +80,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f32x2 splat2(float v) { return (f32x2){v, v}; }
 
-// Two c_gelu evaluations with packed f32 math (v_pk_fma/mul_f32): bit-identical to c_gelu on
-// each element, about half the VALU issue cycles.
-__device__ __forceinline__ f32x2 c_gelu2(f32x2 x) {
+// 2·GELU(x) with the same bits as 2 * c_gelu(x) for every |x| >= 2^-125 (tools/micro/
+// gelu_double_check.c, exhaustive): x + x·tanh(u) in one fma instead of h = x/2, h + h·tanh(u).
+// The encoder kernels feed it to weights pre-scaled by 0.5 on the host (pst_api.cpp, exact for
+// normal weights), so every product (2g)·(w/2) equals g·w and the chains are the canonical ones:
+// one packed multiply less per pair of GELUs. Below 2^-125 the two forms differ by an ulp of a
+// subnormal, a product that cannot change a chain holding anything above ~1e-30.
+__device__ __forceinline__ f32x2 c_gelu2x(f32x2 x) {
   f32x2 u = x * pk_fma(x * x, splat2(GELU_K0K1), splat2(GELU_K0));
   const f32x2 clampv = splat2(7.99881172180175781f);
   f32x2 xc = __builtin_elementwise_min(__builtin_elementwise_max(u, -clampv), clampv);
@@ -97,19 +101,17 @@ __device__ __forceinline__ f32x2 c_gelu2(f32x2 x) {
   f32x2 q = pk_fma(s, splat2(1.19825839466702e-06f), splat2(1.18534705686654e-04f));
   q = pk_fma(s, q, splat2(2.26843463243900e-03f));
   q = pk_fma(s, q, splat2(4.89352518554385e-03f));
-  // division core (see div_tanh), packed
   f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
   f32x2 y = p * r;
   f32x2 e = pk_fma(-q, y, p);
   f32x2 t = pk_fma(e, r, y);
-  f32x2 hx = splat2(0.5f) * x;
-  return pk_fma(hx, t, hx);
+  return pk_fma(x, t, x);
 }
 
-// c_gelu2 with every packed op pinned as v_pk_* by inline asm: the compiler's pre-emit peephole
+// c_gelu2x with every packed op pinned as v_pk_* by inline asm: the compiler's pre-emit peephole
 // otherwise unpacks packed FP32 ops that sit in an MFMA's shadow into two scalar ops each, and on
 // gfx950 that costs VALU issue cycles the MFMA pipe does not hide (A/B on the box: k_mpnn 1.8 %
-// faster pinned; PMC SQ_VALU_MFMA_COEXEC_CYCLES = 0). Same op sequence as c_gelu2, bit for bit.
+// faster pinned; PMC SQ_VALU_MFMA_COEXEC_CYCLES = 0). Same op sequence as c_gelu2x, bit for bit.
 // Constant operands: SGPR pairs holding the constant in both halves (sc2).
 __device__ __forceinline__ uint64_t sc2(float c) { return (uint64_t)__float_as_uint(c) * 0x100000001ull; }
 __device__ __forceinline__ f32x2 apk_mul(f32x2 a, f32x2 b) {
@@ -152,8 +154,9 @@ __device__ __forceinline__ f32x2 apk_fma_neg(f32x2 a, f32x2 b, f32x2 c) {
 // accumulators finished >= 4 MFMA groups earlier. The clamp and the reciprocal stay in C (no
 // packed forms). Measured costs (A/B, 512 x 256 residues): the GELU is ~10 % of k_mpnn, since
 // f32 MFMA and f32 VALU share the vector datapath (MI355X: f32 MFMA peak = vector peak).
+// Returns 2·GELU(x) (c_gelu2x's doubled form, for the half-scaled consumer weights).
 template <bool FRESH>
-__device__ __forceinline__ f32x2 c_gelu2_asm(f32x2 x) {
+__device__ __forceinline__ f32x2 c_gelu2x_asm(f32x2 x) {
   const f32x2 c5 = splat2(2.00018790482477e-13f), q2 = splat2(1.18534705686654e-04f);
   f32x2 u;
   if (FRESH) {
@@ -181,23 +184,22 @@ __device__ __forceinline__ f32x2 c_gelu2_asm(f32x2 x) {
   // covers the one wait state a v_rcp (trans) result needs, which the hazard recognizer does
   // not check for asm operands
   f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
-  f32x2 out, p, y, e, t, hx;
-  asm("v_pk_fma_f32 %1, %7, %10, %11\n\t"
-      "v_pk_fma_f32 %1, %7, %1, %12\n\t"
-      "v_pk_fma_f32 %1, %7, %1, %13\n\t"
-      "v_pk_fma_f32 %1, %7, %1, %14\n\t"
-      "v_pk_fma_f32 %1, %7, %1, %15\n\t"
-      "v_pk_fma_f32 %1, %7, %1, %16\n\t"
-      "v_pk_mul_f32 %1, %6, %1\n\t"
-      "v_pk_mul_f32 %2, %1, %8\n\t"
-      "v_pk_fma_f32 %3, %9, %2, %1 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-      "v_pk_fma_f32 %4, %3, %8, %2\n\t"
-      "v_pk_mul_f32 %5, %17, %18\n\t"
-      "v_pk_fma_f32 %0, %5, %4, %5"
-      : "=&v"(out), "=&v"(p), "=&v"(y), "=&v"(e), "=&v"(t), "=&v"(hx)
+  f32x2 out, p, y, e, t;
+  asm("v_pk_fma_f32 %1, %6, %9, %10\n\t"
+      "v_pk_fma_f32 %1, %6, %1, %11\n\t"
+      "v_pk_fma_f32 %1, %6, %1, %12\n\t"
+      "v_pk_fma_f32 %1, %6, %1, %13\n\t"
+      "v_pk_fma_f32 %1, %6, %1, %14\n\t"
+      "v_pk_fma_f32 %1, %6, %1, %15\n\t"
+      "v_pk_mul_f32 %1, %5, %1\n\t"
+      "v_pk_mul_f32 %2, %1, %7\n\t"
+      "v_pk_fma_f32 %3, %8, %2, %1 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+      "v_pk_fma_f32 %4, %3, %7, %2\n\t"
+      "v_pk_fma_f32 %0, %16, %4, %16"
+      : "=&v"(out), "=&v"(p), "=&v"(y), "=&v"(e), "=&v"(t)
       : "v"(xc), "v"(sq), "v"(r), "v"(q), "s"(sc2(-2.76076847742355e-16f)), "v"(c5),
         "s"(sc2(-8.60467152213735e-11f)), "s"(sc2(5.12229709037114e-08f)), "s"(sc2(1.48572235717979e-05f)),
-        "s"(sc2(6.37261928875436e-04f)), "s"(sc2(4.89352455891786e-03f)), "v"(x), "s"(sc2(0.5f)));
+        "s"(sc2(6.37261928875436e-04f)), "s"(sc2(4.89352455891786e-03f)), "v"(x));
   return out;
 }
 
@@ -535,12 +537,12 @@ struct ActId {
   __device__ __forceinline__ f32x2 operator()(int, f32x2 x) const { return x; }
 };
 
-// GELU of the previous layer's output (its bias is already in the accumulator: chains start
-// from the bias)
-struct ActGelu {
+// 2·GELU of the previous layer's output (its bias is already in the accumulator: chains start
+// from the bias); the consuming weights are pre-scaled by 0.5 (c_gelu2x)
+struct ActGelu2x {
   __device__ __forceinline__ f32x2 operator()(int t, f32x2 x) const {
     // the first group's pairs are evaluated right after the GEMM that produced them (FRESH)
-    return t < ACT_GROUP ? c_gelu2_asm<true>(x) : c_gelu2_asm<false>(x);
+    return t < ACT_GROUP ? c_gelu2x_asm<true>(x) : c_gelu2x_asm<false>(x);
   }
 };
 

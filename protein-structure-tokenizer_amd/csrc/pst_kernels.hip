@@ -432,8 +432,8 @@ __device__ __forceinline__ void tile_add_row(Tile& acc, const float* __restrict_
 // applied just in time inside the next GEMM.
 __device__ __forceinline__ void mlp3_tail(Tile& acc, const MlpW& W) {
   Tile a2;
-  tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu{});
-  tile_gemm_bf(acc, a2, W.w2, W.bf2, ActGelu{});
+  tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu2x{});
+  tile_gemm_bf(acc, a2, W.w2, W.bf2, ActGelu2x{});
 }
 __device__ __forceinline__ void mlp3(Tile& acc, const Tile& X, const MlpW& W) {
   tile_gemm(acc, X, W.w0);
@@ -461,9 +461,9 @@ template <int KL = 0>
 __device__ __forceinline__ void msg_hidden(Tile& acc, const MlpW& W, const float4* w1_lds = nullptr) {
   Tile a2;
   if (KL > 0 && w1_lds)
-    tile_gemm_mix_bf<(KL > 0 ? KL : 1)>(a2, acc, w1_lds, W.w1, W.bf1, ActGelu{});
+    tile_gemm_mix_bf<(KL > 0 ? KL : 1)>(a2, acc, w1_lds, W.w1, W.bf1, ActGelu2x{});
   else
-    tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu{});
+    tile_gemm_bf(a2, acc, W.w1, W.bf1, ActGelu2x{});
   __builtin_amdgcn_sched_barrier(0);
   // 20 wait states: the packed GELU's asm reads the accumulators the last MFMAs just wrote,
   // and only the compiler's hazard recognizer would otherwise space them
@@ -472,7 +472,7 @@ __device__ __forceinline__ void msg_hidden(Tile& acc, const MlpW& W, const float
   for (int M = 0; M < 4; ++M)
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
-      const f32x2 v = c_gelu2_asm<false>((f32x2){a2.m[M][r], a2.m[M][r + 1]});
+      const f32x2 v = c_gelu2x_asm<false>((f32x2){a2.m[M][r], a2.m[M][r + 1]});
       acc.m[M][r] = v.x;
       acc.m[M][r + 1] = v.y;
     }
@@ -643,9 +643,9 @@ __device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t
     Tile hid;
     tile_gemm_bf(hid, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, ActId{});
     if (ck == 0)
-      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu{});
+      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu2x{});
     else
-      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu{});
+      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu2x{});
   }
   tile_add(x, out);
   tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
@@ -763,9 +763,9 @@ __device__ __forceinline__ void mpnn_node_tile(const MpnnArgs& a, int64_t g0, in
     Tile hid;
     tile_gemm_bf(hid, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, ActId{});
     if (ck == 0)
-      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu{});
+      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu2x{});
     else
-      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu{});
+      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu2x{});
   }
   tile_add(x, out);
   tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
@@ -949,9 +949,9 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
     Tile hid;
     tile_gemm_bf(hid, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, ActId{});
     if (ck == 0)
-      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu{});
+      tile_gemm_bf(out, hid, a.ff_w2, a.ff_bf2, ActGelu2x{});
     else
-      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu{});
+      tile_gemm_f(out, hid, a.ff_w2 + ck * 64 * 64, ActGelu2x{});
   }
   tile_add(x, out);
   tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
@@ -1801,8 +1801,8 @@ __device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, 
       blk_gemm_bf(h1, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, b1, ActId{});
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
-        const f32x2 v0 = c_gelu2((f32x2){h0[r], h0[r + 1]});
-        const f32x2 v1 = c_gelu2((f32x2){h1[r], h1[r + 1]});
+        const f32x2 v0 = c_gelu2x((f32x2){h0[r], h0[r + 1]});
+        const f32x2 v1 = c_gelu2x((f32x2){h1[r], h1[r + 1]});
         h0[r] = v0.x;
         h0[r + 1] = v0.y;
         h1[r] = v1.x;
@@ -1891,7 +1891,7 @@ __global__ __launch_bounds__(256, 1) void k_mpnn_node_coop(MpnnArgs a) {
     blk_gemm_bf(h1, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, w, ActId{});
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
-      const f32x2 v = c_gelu2((f32x2){h1[r], h1[r + 1]});
+      const f32x2 v = c_gelu2x((f32x2){h1[r], h1[r + 1]});
       h1[r] = v.x;
       h1[r + 1] = v.y;
     }

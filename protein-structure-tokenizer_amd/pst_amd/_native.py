@@ -40,7 +40,8 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_pdb_batch_sizes", "pst_pdb_batch_copy", "pst_pdb_batch_error", "pst_pdb_batch_free", "pst_write_files",
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
            "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_decode_ex", "pst_decoder_debug",
-           "pst_build_graph", "pst_clock_counters", "pst_set_clock_counters", "pst_pdb_batch_copy_f32")
+           "pst_build_graph", "pst_clock_counters", "pst_set_clock_counters", "pst_pdb_batch_copy_f32",
+           "pst_decoder_set_timing", "pst_decoder_get_timing")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -90,6 +91,8 @@ def lib():
         L.pst_device_count.argtypes = [P]
         L.pst_clock_counters.argtypes = [P, P, ctypes.c_int32]
         L.pst_set_clock_counters.argtypes = [P, ctypes.c_int32]
+        L.pst_decoder_set_timing.argtypes = [P, ctypes.c_int32]
+        L.pst_decoder_get_timing.argtypes = [P, P]
         L.pst_pdb_parse_files.argtypes = [P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_parse_strings.argtypes = [P, P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_batch_sizes.argtypes = [P, P, P]
@@ -468,3 +471,13 @@ class Decoder:
         out = np.zeros(n_floats, np.float32)
         self._check(lib().pst_decoder_debug(self._h, which, _ptr(out), n_floats))
         return out
+
+    def set_timing(self, on: bool = True):
+        """Stage timing (pst_decoder_set_timing): direct launches with HIP events while on."""
+        self._check(lib().pst_decoder_set_timing(self._h, 1 if on else 0))
+
+    def stage_ms(self) -> dict:
+        """ms per stage summed since set_timing(True): upsampler, pair inputs, k_pair_fused, fold."""
+        ms = np.zeros(4, np.float32)
+        self._check(lib().pst_decoder_get_timing(self._h, _ptr(ms)))
+        return dict(zip(("upsampler", "pair_inputs", "k_pair_fused", "fold"), ms.tolist()))

@@ -39,3 +39,18 @@ def test_gelu_matches_jax_formula():
     x = xs.astype(np.float64)
     ref = x * 0.5 * (1 + np.tanh(np.sqrt(2 / np.pi) * (x + 0.044715 * x ** 3)))
     assert np.abs(got - ref).max() < 2e-6
+
+
+def test_doubled_gelu_identity(tmp_path):
+    """The encoder kernels evaluate 2·GELU(x) as x + x·tanh(u) (one fma less than h + h·tanh(u))
+    and feed it to weights pre-scaled by 0.5 (pst_device.h c_gelu2x, pst_api.cpp): exact iff
+    fma(x, t, x) == 2·fma(x/2, t, x/2) bitwise. tools/micro/gelu_double_check.c checks every
+    float32 input (no mismatch for |x| >= 2^-125); here every 101st input."""
+    import os
+    import subprocess
+    src = os.path.join(os.path.dirname(__file__), "..", "tools", "micro", "gelu_double_check.c")
+    exe = str(tmp_path / "gdc")
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-mfma", "-DSTRIDE=101", src, "-o", exe, "-lm"], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, env=dict(os.environ, OMP_NUM_THREADS="4"))
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert " 0 mismatches with |x| >= 2^-125" in out.stdout, out.stdout

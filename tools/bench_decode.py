@@ -36,7 +36,26 @@ for _ in range(a.reps):
     out = dec.decode(toks)
 dt = (time.perf_counter() - t0) / a.reps
 N = a.tokens * a.df
+# stage times (HIP events on the decoder's stream, direct launches) and the dominant kernel's
+# roofline: k_pair_fused executes MFMA_PER_PAIR_TILE v_mfma_f32_32x32x2_f32 per 32-pair tile
+# (pst_decode.hip k_pair_fused: 13 K=128 tile GEMMs x 256 — out1 x4, out2 x2, right1 x2, seq_linear,
+# pt1 x2, pt2 x2 — + 2 bias k-step groups x 4 + the 64-step narrow attention-bias GEMM = 3 400)
+MFMA_PER_PAIR_TILE = 13 * 256 + 2 * 4 + 64
+PEAK_FP32_TFLOPS = 157.3
+dec.set_timing(True)
+for _ in range(a.reps):
+    dec.decode(toks)
+st = {k: v / a.reps for k, v in dec.stage_ms().items()}
+dec.set_timing(False)
+tiles = a.proteins * ((N * N + 31) // 32)  # one group: pairs of each protein, 32-pair tiles
+ex = tiles * MFMA_PER_PAIR_TILE * 32 * 32 * 2 * 2 / (st["k_pair_fused"] * 1e-3) / 1e12
 print(json.dumps({"path": "decode (tokens -> backbone atom37)", "proteins": a.proteins, "tokens_per_protein": a.tokens,
                   "residues_per_protein": N, "codebook": a.codebook, "df": a.df, "ms_per_batch": round(dt * 1e3, 2),
-                  "residues_per_s": round(a.proteins * N / dt, 1), "finite": bool(all(np.isfinite(o).all() for o in out))}))
+                  "residues_per_s": round(a.proteins * N / dt, 1), "finite": bool(all(np.isfinite(o).all() for o in out)),
+                  "stage_ms": {k: round(v, 3) for k, v in st.items()},
+                  "roofline": {"kernel": "k_pair_fused (pair chain of the sequence decoder + structure-module pair inputs)",
+                               "bound": "mfma", "achieved": round(ex, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(ex / PEAK_FP32_TFLOPS, 4), "mfma_per_32_pair_tile": MFMA_PER_PAIR_TILE,
+                               "launch_ms": round(st["k_pair_fused"], 3),
+                               "note": "executed f32 MFMA FLOPs / HIP-event launch time (timed pass without graph replay)"}}))
 dec.close()
