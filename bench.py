@@ -45,11 +45,11 @@ SPEC_GHZ = 2.4             # the shader clock the peak is quoted at
 H, K = 128, 50
 MFMA_FLOP = 32 * 32 * 2 * 2  # one v_mfma_f32_32x32x2_f32
 # MFMA instructions per 32-receiver task (equal to the PMC SQ_INSTS_MFMA per launch
-# / (R/32), profiles/r02_pmc_mfma.txt): per 32-edge block k_mpnn<0> 388 (edge embed 64 +
-# message first layer 64 + W1 65·4), k_mpnn<1,2> 1292 (edge MLP 64·4 + 65·4 + 65·4, message MLP
-# 64·4 + 65·4); node part: message W2 after the segment sum 256, FFN 2068, projections 1032
-# (layers 0, 1 only).
-MFMA_PER_TASK = {"mpnn0": 50 * 380 + 256 + 2068 + 1032, "mpnn1": 50 * 1292 + 256 + 2068 + 1032,
+# / (R/32), profiles/r02_pmc_mfma.txt): per 32-edge block k_mpnn<0> 372 (edge embed 14·4 +
+# message first layer 14·4 over the 27 features in 14 k-steps + W1 65·4; 380 with 15 k-steps
+# before round 5), k_mpnn<1,2> 1292 (edge MLP 64·4 + 65·4 + 65·4, message MLP 64·4 + 65·4); node
+# part: message W2 after the segment sum 256, FFN 2068, projections 1032 (layers 0, 1 only).
+MFMA_PER_TASK = {"mpnn0": 50 * 372 + 256 + 2068 + 1032, "mpnn1": 50 * 1292 + 256 + 2068 + 1032,
                  "mpnn2": 50 * 1292 + 256 + 2068}
 # SURVEY §8d algorithmic FLOPs (padding and dead code removed) of k_mpnn<1>'s work: edge MLP of
 # layer 1 + message MLP of layer 2 over 50 edges + the layer-2 node FFN

@@ -319,7 +319,15 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   HostParams P;
   walk(blob, ctx->D, &P);
   Arena A;
-  ctx->emb_w = A.add(frag(P.edge_embed.w, H, 128, 27, 32, 0, 128));
+  // the feature rows of the edge embedding and of layer 0's message factor in the slot order of
+  // the features k_knn writes (pst::feat_slot; unused slots zero)
+  auto slot_rows = [&](const float* W) {
+    std::vector<float> S((size_t)32 * H, 0.0f);
+    for (int f = 0; f < pst::FEAT_USED; ++f)
+      std::copy(W + (size_t)f * H, W + (size_t)(f + 1) * H, S.begin() + (size_t)pst::feat_slot(f) * H);
+    return S;
+  };
+  ctx->emb_w = A.add(frag(slot_rows(P.edge_embed.w + (size_t)128 * H).data(), H, 0, 32, 32, 0, 128));
   ctx->emb_b = A.add(perm(P.edge_embed.b));
   {
     // layer-0 message over the embedding's feature factor: Wm[f] = Wf[f] · msg0
@@ -338,7 +346,7 @@ int build_weights(pst_ctx* ctx, const float* blob) {
         Wm[(size_t)f * H + o] = acc;
       }
     }
-    ctx->w_msg0f = A.add(frag(Wm.data(), H, 0, 27, 32, 0, 128));
+    ctx->w_msg0f = A.add(frag(slot_rows(Wm.data()).data(), H, 0, 32, 32, 0, 128));
   }
   for (int l = 0; l < 3; ++l) {
     const Layer& S = P.L[l];
@@ -1211,7 +1219,7 @@ int pst_build_graph(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_fl
       for (int j = 0; j < KNN; ++j) {
         const size_t e = (size_t)g * KNN + j;
         senders_out[e] = real && snd[e] >= 0 ? (int32_t)(snd[e] - base) : -1;
-        for (int c = 0; c < 27; ++c) edge_features_out[e * 27 + c] = real ? feat[e * 32 + c] : 0.0f;
+        for (int c = 0; c < 27; ++c) edge_features_out[e * 27 + c] = real ? feat[e * 32 + pst::feat_slot(c)] : 0.0f;
       }
       if (!real) ca_out[3 * g] = ca_out[3 * g + 1] = ca_out[3 * g + 2] = 0.0;
     }
@@ -1386,9 +1394,15 @@ int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes) {
           for (int r = 0; r < 16; ++r) o[i * 128 + tile_channel(h, M, r)] = tmp[i * 128 + h * 64 + M * 16 + r];
     return PST_OK;
   }
-  if (which == 10) {
-    src = ctx->w.feat;
+  if (which == 10) {  // 32-float rows in feature order (features 0..26, then +0), from feat_slot's
     need = (size_t)ctx->last_R * KNN * 32 * sizeof(float);
+    if (bytes < need) return fail(ctx, PST_E_INVALID, "debug buffer too small");
+    tmp.resize(need / sizeof(float));
+    HIPCHK(hipMemcpy(tmp.data(), ctx->w.feat, need, hipMemcpyDeviceToHost));
+    float* o = (float*)out;
+    for (size_t e = 0; e < (size_t)ctx->last_R * KNN; ++e)
+      for (int f = 0; f < 32; ++f) o[e * 32 + f] = f < pst::FEAT_USED ? tmp[e * 32 + pst::feat_slot(f)] : 0.0f;
+    return PST_OK;
   } else if (which == 11) {
     src = ctx->w.senders;
     need = (size_t)ctx->last_R * KNN * sizeof(int32_t);

@@ -182,7 +182,11 @@ __device__ __forceinline__ f32x2 c_gelu2x_asm(f32x2 x) {
         "s"(sc2(4.89352518554385e-03f)));
   // the reciprocal issues here, 7 instructions before its first use in the next group: that
   // covers the one wait state a v_rcp (trans) result needs, which the hazard recognizer does
-  // not check for asm operands
+  // not check for asm operands. The block ends with s_nop 1: its output is the B operand of the
+  // next MFMAs, and an MFMA reading a VGPR a VALU wrote needs 2 wait states that hipcc does not
+  // insert after inline asm (round 5: without it k_mpnn_q<1,4> read a stale operand — its MFMA
+  // followed the final fma one instruction later — while every other instantiation happened to
+  // be scheduled far enough apart; tools/mfma_hazard_scan.py checks the built code objects)
   f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
   f32x2 out, p, y, e, t;
   asm("v_pk_fma_f32 %1, %6, %9, %10\n\t"
@@ -195,7 +199,8 @@ __device__ __forceinline__ f32x2 c_gelu2x_asm(f32x2 x) {
       "v_pk_mul_f32 %2, %1, %7\n\t"
       "v_pk_fma_f32 %3, %8, %2, %1 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
       "v_pk_fma_f32 %4, %3, %7, %2\n\t"
-      "v_pk_fma_f32 %0, %16, %4, %16"
+      "v_pk_fma_f32 %0, %16, %4, %16\n\t"
+      "s_nop 1"  // VALU write -> MFMA operand read: 2 wait states, which hipcc does not pad for asm
       : "=&v"(out), "=&v"(p), "=&v"(y), "=&v"(e), "=&v"(t)
       : "v"(xc), "v"(sq), "v"(r), "v"(q), "s"(sc2(-2.76076847742355e-16f)), "v"(c5),
         "s"(sc2(-8.60467152213735e-11f)), "s"(sc2(5.12229709037114e-08f)), "s"(sc2(1.48572235717979e-05f)),

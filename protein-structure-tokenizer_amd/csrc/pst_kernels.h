@@ -5,6 +5,16 @@
 
 namespace pst {
 
+// Storage slot of edge feature f (0..26) in the 32-float feature rows k_knn writes. The feature
+// GEMMs read slot (r&3) + 8(r>>2) + 4h at k-step r, lane half h (the MFMA k order, half 0 first),
+// so the chain visits the real features in the order f0, f4, f1, f5, …, f23 (k-steps 0..11), then
+// f24, f25 (k-step 12) and f26 (k-step 13, slot 25; its partner slot 29 is +0): the same order the
+// identity layout visited them in, with its zero padding interleaved there. Padding adds +-0
+// products, which leave a nonzero chain unchanged, so k-steps 14 and 15 (only padding) are
+// skipped with identical results. Slots 26, 27, 29, 30 and 31 hold +0.
+__host__ __device__ constexpr int feat_slot(int f) { return f == 25 ? 28 : f == 26 ? 25 : f; }
+constexpr int FEAT_USED = 27;
+
 struct PrepArgs {
   const double* pos;       // [R,37,3]
   const uint8_t* flags;    // [R,37]

@@ -170,11 +170,15 @@ __device__ void edge_features(const double* fr_r, const double* fr_s, const doub
     f[21 + j] = (float)dot3(row, fr_s + 3);
     f[24 + j] = (float)dot3(row, fr_s + 6);
   }
+  // stored in the feature GEMMs' slot order (feat_slot), padding slots +0
+  float g[32];
 #pragma unroll
-  for (int j = 27; j < 32; ++j) f[j] = 0.0f;
+  for (int j = 0; j < 32; ++j) g[j] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < FEAT_USED; ++j) g[feat_slot(j)] = f[j];
   float4* o = reinterpret_cast<float4*>(out);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) o[q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+  for (int q = 0; q < 8; ++q) o[q] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
 }
 
 __device__ __forceinline__ bool lex_less(double d1, int s1, double d2, int s2) {
@@ -492,18 +496,19 @@ __device__ __forceinline__ void agg_from_gsum(Tile& ag, const float* __restrict_
   tile_gemm(ag, G, W.w2);
 }
 
-// acc += x[features] · Wf over the 32 (27 + zero pad) edge features, 16 MFMA k-steps;
-// x[r] holds features (r&3) + 8(r>>2) + 4·half (the k order of the fragments)
+// acc += x[slots] · Wf over the 27 edge features in 32 slots (feat_slot, pst_kernels.h);
+// x[r] holds slots (r&3) + 8(r>>2) + 4·half (the k order of the fragments)
 // (fragments through a buffer resource with constant SGPR offsets and a FEAT_DEPTH-deep register
 // ring, as tile_gemm_f: no per-k-step 64-bit addresses; k_mpnn<0> 8.60 -> 8.45 ms)
-// k-step 15 holds features 27 and 31, both zero padding (edge_features writes +0.0f there), so
-// it is skipped: its four MFMAs would add +-0 products to the chains (no change to a nonzero sum;
-// FEAT_KSTEPS=16 restores them for A/B)
+// k-steps 14 and 15 hold only zero padding (slots 26, 27, 30, 31; feat_slot packs the 27 features
+// into k-steps 0..13), so they are skipped: their MFMAs would add +-0 products to the chains (no
+// change to a nonzero sum). Round 2 skipped k-step 15 (8.36 -> 8.29 ms); round 5 moved features
+// 25 and 26 into slots 28 and 25 (same chain order) so k-step 14 goes too.
 #ifndef FEAT_DEPTH
 #define FEAT_DEPTH 4
 #endif
 #ifndef FEAT_KSTEPS
-#define FEAT_KSTEPS 15
+#define FEAT_KSTEPS 14
 #endif
 // ST: also write tile E out blocked through `st`, quad r at k-step r (the rest after the loop),
 // spread as in tile_gemm_store
@@ -565,7 +570,7 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
   float x[16];  // layer 0: this lane's edge features
   int lr0 = 0, ls0 = 0;
   if (LAYER == 0) {
-    // init_edge_embed: chain from T[s-r] (= b + edgePE(s-r) W[0:128]) over the 27 (+5 zero) features.
+    // init_edge_embed: chain from T[s-r] (= b + edgePE(s-r) W[0:128]) over the 27 features.
     // A protein's nodes sit in consecutive slots (slot = protein base + local index, k_prep), so
     // ls - lr = s - g without reading node_local[s]; gap/padding receivers have self edges
     // (s = g) and lr clamped to 0, hence ls = 0 as before. The T row then needs no load at all.

@@ -40,7 +40,7 @@ namespace {
 struct Parsed {
   int status = PST_OK;
   std::string error;
-  std::vector<double> pos;     // [n,37,3]
+  std::vector<float> pos;      // [n,37,3] (Bio's float32 atom.coord)
   std::vector<uint8_t> flags;  // [n,37]
   std::vector<uint8_t> aatype; // [n]
   int64_t n = 0;
@@ -136,6 +136,35 @@ inline bool parse_double(Field f, double* v) {
   return true;
 }
 
+// Coordinate field [a, a+8) in the fixed "%8.3f" form PDB writers emit (right-aligned, '.' at
+// a+4, three decimals, e.g. "  -12.345"): the integer m = value x 1000 and one IEEE division —
+// the correctly rounded double, as parse_double's generic path and strtod give. false = not that
+// form (the caller falls back to field() + parse_double, which also handles every other form).
+inline bool coord_fixed(const char* line, int len, int a, double* v) {
+  if (a + 8 > len || line[a + 4] != '.') return false;
+  const char* p = line + a;
+  const unsigned d5 = (unsigned)(p[5] - '0'), d6 = (unsigned)(p[6] - '0'), d7 = (unsigned)(p[7] - '0');
+  if (d5 > 9 || d6 > 9 || d7 > 9) return false;
+  int i = 0;
+  while (i < 4 && p[i] == ' ') ++i;
+  bool neg = false;
+  if (i < 4 && (p[i] == '-' || p[i] == '+')) {
+    neg = p[i] == '-';
+    ++i;
+  }
+  if (i == 4) return false;  // no integer digit (".123", "-.123": the generic path)
+  int64_t m = 0;
+  for (; i < 4; ++i) {
+    const unsigned d = (unsigned)(p[i] - '0');
+    if (d > 9) return false;
+    m = m * 10 + d;
+  }
+  m = (m * 10 + d5) * 100 + d6 * 10 + d7;
+  const double r = (double)m / 1000.0;
+  *v = neg ? -r : r;
+  return true;
+}
+
 // ---- atom37 name lookup: the stripped 1-4 character name packed little-endian into a uint32,
 // found in a 128-entry open-addressing table built once
 inline uint32_t pack_name(const char* p, int n) {
@@ -169,9 +198,21 @@ const AtomTable& atom_table() {
   return t;
 }
 
+// residue type of a stripped residue name: its packed little-endian bytes (pack_name) against the
+// 20 standard names packed once (a name of 4+ characters never matches: pack_name keeps 4 bytes,
+// and a 3-letter name packs with a zero 4th byte)
 int restype_index(Field resname) {
+  struct Names {
+    uint32_t k[20];
+    Names() {
+      for (int r = 0; r < 20; ++r) k[r] = pack_name(pst::kResName3[r], 3);
+    }
+  };
+  static const Names N;
+  if (resname.n != 3) return 20;
+  const uint32_t key = pack_name(resname.p, 3);
   for (int r = 0; r < 20; ++r)
-    if (resname.eq(pst::kResName3[r])) return r;
+    if (N.k[r] == key) return r;
   return 20;
 }
 
@@ -182,9 +223,10 @@ struct Res {
   int resseq;
   char icode;
   uint8_t restype;
-  uint64_t present;  // bit a: atom37 slot a filled
+  uint64_t present;  // bit a: atom37 slot a filled (xyz / occ of slot a are set only then)
   float xyz[pst::kAtomTypes][3];
   double occ[pst::kAtomTypes];
+  Res() {}  // no zero fill of the 740-byte slot arrays: only the present slots are ever read
 };
 
 struct Chain {
@@ -257,8 +299,10 @@ void scan_chunk(const char* text, size_t len, size_t p0, size_t p1, std::vector<
     r.icode = 26 < ll ? line[26] : ' ';
     int resseq;
     double x = 0.0, y = 0.0, z = 0.0, occ = 0.0;
-    if (!parse_int(field(line, ll, 22, 26), &resseq) || !parse_double(field(line, ll, 30, 38), &x) ||
-        !parse_double(field(line, ll, 38, 46), &y) || !parse_double(field(line, ll, 46, 54), &z)) {
+    if (!parse_int(field(line, ll, 22, 26), &resseq) ||
+        !(coord_fixed(line, ll, 30, &x) || parse_double(field(line, ll, 30, 38), &x)) ||
+        !(coord_fixed(line, ll, 38, &y) || parse_double(field(line, ll, 38, 46), &y)) ||
+        !(coord_fixed(line, ll, 46, &z) || parse_double(field(line, ll, 46, 54), &z))) {
       r.kind = R_BAD_COORD;
       out->push_back(r);
       continue;
@@ -270,8 +314,9 @@ void scan_chunk(const char* text, size_t len, size_t p0, size_t p1, std::vector<
       continue;
     }
     r.resseq = resseq;
-    r.het = is_het ? ((resname.eq("HOH") || resname.eq("WAT")) ? 1 : 2) : 0;
     r.resname = pack_name(resname.p, resname.n);
+    r.het = is_het ? ((resname.n == 3 && (r.resname == pack_name("HOH", 3) || r.resname == pack_name("WAT", 3))) ? 1 : 2)
+                   : 0;
     r.restype = (uint8_t)restype_index(resname);
     r.atom = (int8_t)(name.n >= 1 && name.n <= 4 ? T.find(pack_name(name.p, name.n)) : -1);
     r.xyz[0] = (float)x;
@@ -390,7 +435,7 @@ void assemble(const char* text, size_t len, const std::vector<std::vector<Rec>>&
       n_keep += r.present != 0;
     }
   }
-  out->pos.resize(n_keep * pst::kAtomTypes * 3);
+  out->pos.assign(n_keep * pst::kAtomTypes * 3, 0.0f);
   out->flags.resize(n_keep * pst::kAtomTypes);
   out->aatype.resize(n_keep);
   size_t k = 0;
@@ -399,14 +444,15 @@ void assemble(const char* text, size_t len, const std::vector<std::vector<Rec>>&
     for (int ri : ch.residues) {
       const Res& r = res[ri];
       if (!r.present) continue;  // no atom37 atom: skipped (protein_structure_sample.py:228-230)
-      double* pos = out->pos.data() + k * pst::kAtomTypes * 3;
+      float* pos = out->pos.data() + k * pst::kAtomTypes * 3;
       uint8_t* fl = out->flags.data() + k * pst::kAtomTypes;
-      for (int a = 0; a < pst::kAtomTypes; ++a) {
-        const bool has = (r.present >> a) & 1;
-        pos[3 * a + 0] = has ? (double)r.xyz[a][0] : 0.0;
-        pos[3 * a + 1] = has ? (double)r.xyz[a][1] : 0.0;
-        pos[3 * a + 2] = has ? (double)r.xyz[a][2] : 0.0;
-        fl[a] = (uint8_t)((has ? 1 : 0) | (pst::kResAtomExists[r.restype][a] << 1));
+      for (int a = 0; a < pst::kAtomTypes; ++a) fl[a] = (uint8_t)(pst::kResAtomExists[r.restype][a] << 1);
+      for (uint64_t m = r.present; m; m &= m - 1) {  // the present slots (absent ones stay 0)
+        const int a = __builtin_ctzll(m);
+        pos[3 * a + 0] = r.xyz[a][0];
+        pos[3 * a + 1] = r.xyz[a][1];
+        pos[3 * a + 2] = r.xyz[a][2];
+        fl[a] |= 1;
       }
       out->aatype[k] = r.restype;
       ++k;
@@ -507,8 +553,8 @@ void parse_texts(int32_t n, const char* const* texts, const size_t* lens, char c
 }  // namespace
 
 namespace {
-// positions as double (pst_pdb_batch_copy) or float (pst_pdb_batch_copy_f32: the parser's values are
-// float32 already, Bio's atom.coord, so the float copy is exact and half the bytes)
+// positions as float (pst_pdb_batch_copy_f32: the parser's values are Bio's float32 atom.coord,
+// copied as they are) or double (pst_pdb_batch_copy: widened, exact)
 template <typename T>
 int batch_copy(const pst_pdb_batch* b, T* positions, uint8_t* flags, uint8_t* aatype, int64_t* offsets,
                int32_t* status) {
@@ -519,18 +565,18 @@ int batch_copy(const pst_pdb_batch* b, T* positions, uint8_t* flags, uint8_t* aa
   if (offsets) memcpy(offsets, off.data(), sizeof(int64_t) * (n + 1));
   for (int32_t i = 0; i < n; ++i)
     if (status) status[i] = b->items[i].status;
-  // the copies (~925 B per residue) on a few threads once there are megabytes of them
-  // (the float32 form converts element by element: threads from 1 MB on)
+  // the copies (~481 B per residue as float32) on a few threads once there are megabytes of them
+  // (the float64 form widens element by element: threads from 1 MB on)
   const int64_t bytes = off[n] * (37 + 111 * (int64_t)sizeof(T));
-  const int threads = bytes > (sizeof(T) == sizeof(double) ? (4 << 20) : (1 << 20)) ? 8 : 1;
+  const int threads = bytes > (sizeof(T) == sizeof(float) ? (4 << 20) : (1 << 20)) ? 8 : 1;
   run_pool(n, threads, [&](int i) { return (size_t)b->items[i].n; }, [&](int i) {
     const Parsed& it = b->items[i];
     const int64_t r = off[i];
     if (positions && it.n) {
-      if (sizeof(T) == sizeof(double)) {
-        memcpy(positions + r * 111, it.pos.data(), sizeof(double) * 111 * it.n);
+      if (sizeof(T) == sizeof(float)) {
+        memcpy(positions + r * 111, it.pos.data(), sizeof(float) * 111 * it.n);
       } else {
-        const double* src = it.pos.data();
+        const float* src = it.pos.data();
         T* dst = positions + r * 111;
         for (int64_t k = 0; k < 111 * (int64_t)it.n; ++k) dst[k] = (T)src[k];
       }

@@ -90,9 +90,11 @@ def lib():
         L.pst_get_timing.argtypes = [P, P]
         L.pst_device_count.argtypes = [P]
         L.pst_clock_counters.argtypes = [P, P, ctypes.c_int32]
-        L.pst_set_clock_counters.argtypes = [P, ctypes.c_int32]
-        L.pst_decoder_set_timing.argtypes = [P, ctypes.c_int32]
-        L.pst_decoder_get_timing.argtypes = [P, P]
+        # measurement-only entry points: absent from libraries built before round 5 (A/B runs)
+        for name, at in (("pst_set_clock_counters", [P, ctypes.c_int32]),
+                         ("pst_decoder_set_timing", [P, ctypes.c_int32]), ("pst_decoder_get_timing", [P, P])):
+            if hasattr(L, name):
+                getattr(L, name).argtypes = at
         L.pst_pdb_parse_files.argtypes = [P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_parse_strings.argtypes = [P, P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
         L.pst_pdb_batch_sizes.argtypes = [P, P, P]

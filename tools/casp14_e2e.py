@@ -29,6 +29,13 @@ with tempfile.TemporaryDirectory() as d:
             B = parse_pdb_files(files, n_threads=th)
             ts.append(time.perf_counter() - t0)
         out[f"parse_ms_{th}t"] = round(min(ts) * 1e3, 3)
+    for th in (8, 16):
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            B32 = parse_pdb_files(files, n_threads=th, float32=True)
+            ts.append(time.perf_counter() - t0)
+        out[f"parse_f32_ms_{th}t"] = round(min(ts) * 1e3, 3)
     tk = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
     ts = []
     for _ in range(5):
@@ -36,6 +43,16 @@ with tempfile.TemporaryDirectory() as d:
         tok, nt, _ = tk.tokenize_packed(B.positions, B.flags, B.offsets)
         ts.append(time.perf_counter() - t0)
     out["tokenize_ms"] = round(min(ts) * 1e3, 3)
+    # float32 positions (the CLI's wire format) from pageable vs page-locked host memory
+    pin_p = torch.from_numpy(np.ascontiguousarray(B32.positions)).pin_memory().numpy()
+    pin_f = torch.from_numpy(np.ascontiguousarray(B32.flags)).pin_memory().numpy()
+    for name, (pp, pf) in (("tokenize_f32_pageable_ms", (B32.positions, B32.flags)), ("tokenize_f32_pinned_ms", (pin_p, pin_f))):
+        ts = []
+        for _ in range(7):
+            t0 = time.perf_counter()
+            tk.tokenize_packed(pp, pf, B32.offsets)
+            ts.append(time.perf_counter() - t0)
+        out[name] = round(sorted(ts)[3] * 1e3, 3)
     arrs = [tok[int(B.offsets[i]):int(B.offsets[i]) + nt[i]].reshape(1, -1) for i in range(len(files))]
     for th in (1, 4, 16):
         ts = []
