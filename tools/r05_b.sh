@@ -1,6 +1,6 @@
-# Round 5: the doubled-GELU build (one packed multiply less per GELU pair, consumer weights x 0.5,
-# same bits): GPU suite (bitwise vs the oracle), bench line, decode bench with its roofline, PMC
-# instruction counts (VALU / MFMA per launch) for profiles/r05_pmc_summary.txt.
+# Round 5: the doubled-GELU + 14-k-step features + GELU asm hazard guard build (same bits): GPU
+# suite (bitwise vs the oracle), bench line, decode bench with its roofline, CASP14 host probe,
+# PMC instruction counts per launch for profiles/r05_pmc_summary.txt.
 set -e
 TAG=${1:-r05b}
 mkdir -p gpurun_out
@@ -14,6 +14,7 @@ for s in "8 256" "32 128" "8 512"; do
   timeout -k 10 200 python -u tools/bench_decode.py --proteins $1 --tokens $2 >> gpurun_out/${TAG}_decode.jsonl 2>> gpurun_out/${TAG}_decode.err
 done
 echo decode ok
+timeout -k 10 300 python -u tools/casp14_e2e.py > gpurun_out/${TAG}_casp.json 2> gpurun_out/${TAG}_casp.err
 export PST_H2D_CHUNKS=1
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE" "SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES"; do
   t=$(echo $set | cut -d' ' -f1)
