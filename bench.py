@@ -287,7 +287,7 @@ def casp14_end_to_end(tk):
     from host buffers, write <stem>_tokens.npy. Reported beside `value`."""
     import tarfile
     import tempfile
-    from pst_amd._native import parse_pdb_files
+    from pst_amd._native import parse_pdb_files, parse_pdb_files_handle
     from pst_amd.runner import save_npy_files
     arc = os.path.join(ROOT, "tests", "golden", "casp14_pdbs.tar.gz")
     if not os.path.exists(arc):
@@ -305,15 +305,19 @@ def casp14_end_to_end(tk):
             out = os.path.join(d, f"out{rep}")
             os.makedirs(out)
             t0 = time.perf_counter()
-            B = parse_pdb_files(files, n_threads=threads, float32=True)  # exact: Bio's float32 coords
+            H = parse_pdb_files_handle(files, n_threads=threads)  # Bio's float32 coords, kept in libpst
             t1 = time.perf_counter()
-            tok, nt, _ = tk.tokenize_packed(B.positions, B.flags, B.offsets)
+            tok, nt, _ = tk.tokenize_pdb_batch(H)  # page-locked staging inside libpst, pst_tokenize_f32
+            off = H.offsets()
+            H.close()
             t2 = time.perf_counter()
             save_npy_files([os.path.join(out, os.path.basename(f)[:-4] + "_tokens") for f in files],
-                           [tok[int(B.offsets[i]):int(B.offsets[i]) + nt[i]].reshape(1, -1) for i in range(len(files))])
+                           [tok[int(off[i]):int(off[i]) + nt[i]].reshape(1, -1) for i in range(len(files))])
             t3 = time.perf_counter()
             if rep:
                 runs.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2))
+        B = parse_pdb_files(files, n_threads=threads, float32=True)  # arrays for the CPU baseline
+        assert np.array_equal(B.offsets, off)
         R = int(B.offsets[-1])
         casp = (B.positions.astype(np.float64), np.array(B.flags), np.array(B.offsets), (tok.copy(), np.array(nt)))
         tot, parse, tok, write = runs[int(np.argsort([r[0] for r in runs])[len(runs) // 2])]  # median run

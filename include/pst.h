@@ -251,6 +251,13 @@ int pst_pdb_batch_copy_f32(const pst_pdb_batch* b, float* positions, uint8_t* fl
                            int64_t* offsets, int32_t* status);
 const char* pst_pdb_batch_error(const pst_pdb_batch* b, int32_t i);
 void pst_pdb_batch_free(pst_pdb_batch* b);
+/* Tokenize a parsed batch as it stands (the CLI's parse -> tokenize step without a copy through
+ * the caller): the parser's float32 atom37 arrays are packed into the context's page-locked
+ * staging on the host pool and tokenized as pst_tokenize_f32 (same results). Every input must
+ * have parsed: otherwise PST_E_INVALID with that input's parser message (pst_last_error).
+ * tokens_out [R] (R from pst_pdb_batch_sizes), n_tokens_out / n_nodes_out [n] (may be NULL). */
+int pst_tokenize_pdb_batch(pst_ctx* ctx, const pst_pdb_batch* b, uint32_t* tokens_out, int32_t* n_tokens_out,
+                           int32_t* n_nodes_out);
 
 /* Token-file output of the tokenize loop (scripts/inference_runner.py:313-321 writes one
  * np.save per protein): n whole files written (created / truncated) from host buffers on

@@ -291,6 +291,10 @@ struct pst_ctx {
   // 100 MHz ticks] of the stamping wave, Σ wave lifetimes, min wave start, max wave end, waves —
   // summed over calls (min / max over calls)
   unsigned long long* d_clk = nullptr;
+  // page-locked staging of pst_tokenize_pdb_batch (grow-only): positions [R,37,3] f32, flags [R,37]
+  float* h_stage_pos = nullptr;
+  uint8_t* h_stage_flags = nullptr;
+  int64_t h_stage_cap = 0;
   bool clock_on = false;  // pst_set_clock_counters: stamp the fused MPNN launches (off by default)
 };
 
@@ -942,6 +946,8 @@ int pst_destroy(pst_ctx* ctx) {
   for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_U, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
   if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
+  if (ctx->h_stage_pos) (void)hipHostFree(ctx->h_stage_pos);
+  if (ctx->h_stage_flags) (void)hipHostFree(ctx->h_stage_flags);
   for (hipStream_t cs : {ctx->copy_stream, ctx->copy_stream2})
     if (cs) {
       (void)hipStreamSynchronize(cs);
@@ -1184,6 +1190,35 @@ int pst_tokenize(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags
 int pst_tokenize_f32(pst_ctx* ctx, const float* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,
                      int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
   return tokenize_host(ctx, atom_pos, true, atom_flags, offsets, n_prot, tokens_out, n_tokens_out, n_nodes_out);
+}
+
+int pst_tokenize_pdb_batch(pst_ctx* ctx, const pst_pdb_batch* b, uint32_t* tokens_out, int32_t* n_tokens_out,
+                           int32_t* n_nodes_out) {
+  if (!ctx) return PST_E_INVALID;
+  ctx->err.clear();
+  if (!b || !tokens_out) return fail(ctx, PST_E_INVALID, "null batch or token buffer");
+  int32_t n = 0;
+  int64_t R = 0;
+  if (pst_pdb_batch_sizes(b, &n, &R) != PST_OK) return fail(ctx, PST_E_INVALID, "invalid batch");
+  HIPCHK(hipSetDevice(ctx->device));
+  if (R > ctx->h_stage_cap) {
+    if (ctx->h_stage_pos) (void)hipHostFree(ctx->h_stage_pos);
+    if (ctx->h_stage_flags) (void)hipHostFree(ctx->h_stage_flags);
+    ctx->h_stage_pos = nullptr;
+    ctx->h_stage_flags = nullptr;
+    ctx->h_stage_cap = 0;
+    const int64_t cap = std::max<int64_t>(R, 4096);
+    HIPCHK(hipHostMalloc((void**)&ctx->h_stage_pos, sizeof(float) * 111 * cap));
+    HIPCHK(hipHostMalloc((void**)&ctx->h_stage_flags, 37 * cap));
+    ctx->h_stage_cap = cap;
+  }
+  std::vector<int64_t> off(n + 1);
+  std::vector<int32_t> st(n);
+  pst_pdb_batch_copy_f32(b, ctx->h_stage_pos, ctx->h_stage_flags, nullptr, off.data(), st.data());
+  for (int32_t i = 0; i < n; ++i)
+    if (st[i] != PST_OK) return fail(ctx, PST_E_INVALID, pst_pdb_batch_error(b, i));
+  return tokenize_host(ctx, ctx->h_stage_pos, true, ctx->h_stage_flags, off.data(), n, tokens_out, n_tokens_out,
+                       n_nodes_out);
 }
 
 int pst_build_graph(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,

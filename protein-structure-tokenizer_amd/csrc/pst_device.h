@@ -182,30 +182,28 @@ __device__ __forceinline__ f32x2 c_gelu2x_asm(f32x2 x) {
         "s"(sc2(4.89352518554385e-03f)));
   // the reciprocal issues here, 7 instructions before its first use in the next group: that
   // covers the one wait state a v_rcp (trans) result needs, which the hazard recognizer does
-  // not check for asm operands. The block ends with s_nop 1: its output is the B operand of the
-  // next MFMAs, and an MFMA reading a VGPR a VALU wrote needs 2 wait states that hipcc does not
-  // insert after inline asm (round 5: without it k_mpnn_q<1,4> read a stale operand — its MFMA
-  // followed the final fma one instruction later — while every other instantiation happened to
-  // be scheduled far enough apart; tools/mfma_hazard_scan.py checks the built code objects)
+  // not check for asm operands
   f32x2 r = {__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
-  f32x2 out, p, y, e, t;
-  asm("v_pk_fma_f32 %1, %6, %9, %10\n\t"
-      "v_pk_fma_f32 %1, %6, %1, %11\n\t"
-      "v_pk_fma_f32 %1, %6, %1, %12\n\t"
-      "v_pk_fma_f32 %1, %6, %1, %13\n\t"
-      "v_pk_fma_f32 %1, %6, %1, %14\n\t"
-      "v_pk_fma_f32 %1, %6, %1, %15\n\t"
-      "v_pk_mul_f32 %1, %5, %1\n\t"
-      "v_pk_mul_f32 %2, %1, %7\n\t"
-      "v_pk_fma_f32 %3, %8, %2, %1 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-      "v_pk_fma_f32 %4, %3, %7, %2\n\t"
-      "v_pk_fma_f32 %0, %16, %4, %16\n\t"
-      "s_nop 1"  // VALU write -> MFMA operand read: 2 wait states, which hipcc does not pad for asm
-      : "=&v"(out), "=&v"(p), "=&v"(y), "=&v"(e), "=&v"(t)
+  f32x2 p, y, e, t;
+  asm("v_pk_fma_f32 %0, %5, %8, %9\n\t"
+      "v_pk_fma_f32 %0, %5, %0, %10\n\t"
+      "v_pk_fma_f32 %0, %5, %0, %11\n\t"
+      "v_pk_fma_f32 %0, %5, %0, %12\n\t"
+      "v_pk_fma_f32 %0, %5, %0, %13\n\t"
+      "v_pk_fma_f32 %0, %5, %0, %14\n\t"
+      "v_pk_mul_f32 %0, %4, %0\n\t"
+      "v_pk_mul_f32 %1, %0, %6\n\t"
+      "v_pk_fma_f32 %2, %7, %1, %0 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+      "v_pk_fma_f32 %3, %2, %6, %1"
+      : "=&v"(p), "=&v"(y), "=&v"(e), "=&v"(t)
       : "v"(xc), "v"(sq), "v"(r), "v"(q), "s"(sc2(-2.76076847742355e-16f)), "v"(c5),
         "s"(sc2(-8.60467152213735e-11f)), "s"(sc2(5.12229709037114e-08f)), "s"(sc2(1.48572235717979e-05f)),
-        "s"(sc2(6.37261928875436e-04f)), "s"(sc2(4.89352455891786e-03f)), "v"(x));
-  return out;
+        "s"(sc2(6.37261928875436e-04f)), "s"(sc2(4.89352455891786e-03f)));
+  // the last step in C: its output is the B operand of the next MFMAs, and an MFMA reading a VGPR
+  // a VALU just wrote needs 2 wait states that hipcc inserts for its own code but not after inline
+  // asm (round 5: with this fma inside the asm, k_mpnn_q<1,4> read stale operands — its MFMA
+  // followed the fma one instruction later; tools/mfma_hazard_scan.py checks the code objects)
+  return pk_fma(x, t, x);
 }
 
 __device__ __forceinline__ float c_ldexpf(float v, int n) {

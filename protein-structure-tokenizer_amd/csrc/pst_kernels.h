@@ -13,6 +13,10 @@ namespace pst {
 // products, which leave a nonzero chain unchanged, so k-steps 14 and 15 (only padding) are
 // skipped with identical results. Slots 26, 27, 29, 30 and 31 hold +0.
 __host__ __device__ constexpr int feat_slot(int f) { return f == 25 ? 28 : f == 26 ? 25 : f; }
+// the inverse: feature held by slot s, -1 for the zero padding slots
+__host__ __device__ constexpr int slot_feat(int s) {
+  return s < 25 ? s : s == 25 ? 26 : s == 28 ? 25 : -1;
+}
 constexpr int FEAT_USED = 27;
 
 struct PrepArgs {

@@ -153,7 +153,7 @@ __device__ __forceinline__ double dot3(const double* b, const double* x) {
 
 __device__ void edge_features(const double* fr_r, const double* fr_s, const double* ca_r,
                               const double* ca_s, double dist, float* __restrict__ out) {
-  float f[32];
+  float f[FEAT_USED];
   double d2 = dist * dist;
   double ls = 1.0;
 #pragma unroll
@@ -170,15 +170,12 @@ __device__ void edge_features(const double* fr_r, const double* fr_s, const doub
     f[21 + j] = (float)dot3(row, fr_s + 3);
     f[24 + j] = (float)dot3(row, fr_s + 6);
   }
-  // stored in the feature GEMMs' slot order (feat_slot), padding slots +0
-  float g[32];
-#pragma unroll
-  for (int j = 0; j < 32; ++j) g[j] = 0.0f;
-#pragma unroll
-  for (int j = 0; j < FEAT_USED; ++j) g[feat_slot(j)] = f[j];
+  // stored in the feature GEMMs' slot order (feat_slot), padding slots +0 (picked per slot at
+  // compile time: a second 32-float array here cost k_knn 24 VGPRs and three waves per SIMD)
+  auto v = [&](int sl) { return slot_feat(sl) < 0 ? 0.0f : f[slot_feat(sl)]; };
   float4* o = reinterpret_cast<float4*>(out);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) o[q] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+  for (int q = 0; q < 8; ++q) o[q] = make_float4(v(4 * q), v(4 * q + 1), v(4 * q + 2), v(4 * q + 3));
 }
 
 __device__ __forceinline__ bool lex_less(double d1, int s1, double d2, int s2) {

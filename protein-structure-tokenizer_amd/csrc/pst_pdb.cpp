@@ -565,10 +565,9 @@ int batch_copy(const pst_pdb_batch* b, T* positions, uint8_t* flags, uint8_t* aa
   if (offsets) memcpy(offsets, off.data(), sizeof(int64_t) * (n + 1));
   for (int32_t i = 0; i < n; ++i)
     if (status) status[i] = b->items[i].status;
-  // the copies (~481 B per residue as float32) on a few threads once there are megabytes of them
-  // (the float64 form widens element by element: threads from 1 MB on)
+  // the copies (~481 B per residue as float32) on a few threads from a quarter megabyte on
   const int64_t bytes = off[n] * (37 + 111 * (int64_t)sizeof(T));
-  const int threads = bytes > (sizeof(T) == sizeof(float) ? (4 << 20) : (1 << 20)) ? 8 : 1;
+  const int threads = bytes > (256 << 10) ? 8 : 1;  // the pool's workers are hot after the parse
   run_pool(n, threads, [&](int i) { return (size_t)b->items[i].n; }, [&](int i) {
     const Parsed& it = b->items[i];
     const int64_t r = off[i];

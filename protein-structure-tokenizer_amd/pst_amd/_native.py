@@ -41,7 +41,7 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
            "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_decode_ex", "pst_decoder_debug",
            "pst_build_graph", "pst_clock_counters", "pst_set_clock_counters", "pst_pdb_batch_copy_f32",
-           "pst_decoder_set_timing", "pst_decoder_get_timing")
+           "pst_decoder_set_timing", "pst_decoder_get_timing", "pst_tokenize_pdb_batch")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -104,6 +104,7 @@ def lib():
         L.pst_pdb_batch_error.argtypes = [P, ctypes.c_int32]
         L.pst_pdb_batch_free.argtypes = [P]
         L.pst_write_files.argtypes = [ctypes.c_int32, P, P, P, ctypes.c_int32]
+        L.pst_tokenize_pdb_batch.argtypes = [P, P, P, P, P]
         L.pst_decoder_param_count.restype = ctypes.c_size_t
         L.pst_decoder_param_count.argtypes = [ctypes.c_int32]
         L.pst_decoder_create.argtypes = [ctypes.c_int32, ctypes.POINTER(_ModelDesc), P, ctypes.c_size_t, ctypes.POINTER(P)]
@@ -182,6 +183,42 @@ def _collect_pdb(h, f32: bool = False) -> PdbBatch:
     finally:
         L.pst_pdb_batch_free(h)
     return PdbBatch(pos, fl, aa, off, st, errs)
+
+
+class PdbHandle:
+    """A parsed batch kept inside libpst (pst_pdb_parse_files) for Tokenizer.tokenize_pdb_batch:
+    the atom37 arrays go to the GPU without a copy through Python. Free with close()."""
+
+    def __init__(self, h):
+        self._h = h
+        n = ctypes.c_int32()
+        r = ctypes.c_int64()
+        lib().pst_pdb_batch_sizes(h, ctypes.byref(n), ctypes.byref(r))
+        self.n, self.n_residues = n.value, r.value
+
+    def offsets(self) -> np.ndarray:
+        off = np.zeros(self.n + 1, np.int64)
+        lib().pst_pdb_batch_copy_f32(self._h, None, None, None, _ptr(off), None)
+        return off
+
+    def close(self):
+        if self._h:
+            lib().pst_pdb_batch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def parse_pdb_files_handle(paths: Sequence[str], chain_id: Optional[str] = None, n_threads: int = 8) -> PdbHandle:
+    """parse_pdb_files without copying the result out (see PdbHandle)."""
+    enc = [os.fsencode(p) for p in paths]
+    arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+    h = ctypes.c_void_p()
+    rc = lib().pst_pdb_parse_files(arr, len(enc), (chain_id or "\0").encode()[:1], n_threads, ctypes.byref(h))
+    if rc != PST_OK:
+        raise PstError(f"pst_pdb_parse_files failed: {rc}")
+    return PdbHandle(h)
 
 
 def parse_pdb_files(paths: Sequence[str], chain_id: Optional[str] = None, n_threads: int = 8,
@@ -293,6 +330,15 @@ class Tokenizer:
         nn = np.empty(B, np.int32)
         fn = lib().pst_tokenize_f32 if f32 else lib().pst_tokenize
         self._check(fn(self._h, _ptr(pos), _ptr(flags), _ptr(offsets), B, _ptr(tok), _ptr(nt), _ptr(nn)))
+        return tok, nt, nn
+
+    def tokenize_pdb_batch(self, batch: "PdbHandle"):
+        """A parsed batch (parse_pdb_files_handle) → (tokens [R] uint32 raw-offset layout,
+        n_tokens [n], n_nodes [n]) through pst_tokenize_pdb_batch (page-locked staging inside libpst)."""
+        tok = np.empty(max(batch.n_residues, 1), np.uint32)
+        nt = np.empty(batch.n, np.int32)
+        nn = np.empty(batch.n, np.int32)
+        self._check(lib().pst_tokenize_pdb_batch(self._h, batch._h, _ptr(tok), _ptr(nt), _ptr(nn)))
         return tok, nt, nn
 
     def tokenize(self, samples) -> List[np.ndarray]:
