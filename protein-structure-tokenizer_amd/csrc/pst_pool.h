@@ -1,14 +1,10 @@
 // pst_pool.h — one process-wide pool of host worker threads for libpst's host-side work (PDB
 // parsing, token-file writes). Threads are created once and reused: on the GPU boxes a thread
 // start costs tens of microseconds, so a pool per call (three per parse) cost more than the work
-// on a 31-file batch. A worker that finishes a job spins (pause loop) for up to kSpinUs before it
-// blocks on the condition variable again, so the next job of the same CLI step — the parse's
-// second pass, the token-file writes after the GPU call — starts without a futex wake-up per
-// worker (tens of microseconds each on the boxes).
+// on a 31-file batch.
 #pragma once
 #include <algorithm>
 #include <atomic>
-#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -44,7 +40,6 @@ class HostPool {
       next_.store(0);
       pending_ = limit_;
       ++gen_;
-      gen_pub_.store(gen_, std::memory_order_release);
     }
     cv_.notify_all();
     for (int i = next_++; i < n; i = next_++) fn(i);
@@ -57,7 +52,6 @@ class HostPool {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
       ++gen_;
-      gen_pub_.store(gen_, std::memory_order_release);
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
@@ -70,11 +64,6 @@ class HostPool {
       const std::function<void(int)>* job;
       int n;
       {
-        // spin briefly for the next job before sleeping (see the file comment)
-        const auto t0 = std::chrono::steady_clock::now();
-        while (gen_pub_.load(std::memory_order_acquire) == seen &&
-               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kSpinUs))
-          __builtin_ia32_pause();
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
@@ -95,8 +84,6 @@ class HostPool {
   int n_ = 0, limit_ = 0, pending_ = 0;
   std::atomic<int> next_{0};
   uint64_t gen_ = 0;
-  std::atomic<uint64_t> gen_pub_{0};  // gen_, readable without the mutex (the spin)
-  static constexpr int kSpinUs = 4000;
   bool stop_ = false;
 };
 

@@ -90,9 +90,11 @@ def lib():
         L.pst_get_timing.argtypes = [P, P]
         L.pst_device_count.argtypes = [P]
         L.pst_clock_counters.argtypes = [P, P, ctypes.c_int32]
-        # measurement-only entry points: absent from libraries built before round 5 (A/B runs)
+        # entry points added in round 5: absent from older libraries loaded for A/B runs (PST_LIB);
+        # tests/test_abi.py requires every EXPORTS symbol of the in-tree build
         for name, at in (("pst_set_clock_counters", [P, ctypes.c_int32]),
-                         ("pst_decoder_set_timing", [P, ctypes.c_int32]), ("pst_decoder_get_timing", [P, P])):
+                         ("pst_decoder_set_timing", [P, ctypes.c_int32]), ("pst_decoder_get_timing", [P, P]),
+                         ("pst_tokenize_pdb_batch", [P, P, P, P, P])):
             if hasattr(L, name):
                 getattr(L, name).argtypes = at
         L.pst_pdb_parse_files.argtypes = [P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
@@ -104,7 +106,6 @@ def lib():
         L.pst_pdb_batch_error.argtypes = [P, ctypes.c_int32]
         L.pst_pdb_batch_free.argtypes = [P]
         L.pst_write_files.argtypes = [ctypes.c_int32, P, P, P, ctypes.c_int32]
-        L.pst_tokenize_pdb_batch.argtypes = [P, P, P, P, P]
         L.pst_decoder_param_count.restype = ctypes.c_size_t
         L.pst_decoder_param_count.argtypes = [ctypes.c_int32]
         L.pst_decoder_create.argtypes = [ctypes.c_int32, ctypes.POINTER(_ModelDesc), P, ctypes.c_size_t, ctypes.POINTER(P)]
@@ -366,8 +367,10 @@ class Tokenizer:
         self._check(lib().pst_sync(self._h))
 
     def set_clock_counters(self, on: bool = True):
-        """Stamp the fused MPNN launches into the clock counters (off by default: measurement only)."""
-        self._check(lib().pst_set_clock_counters(self._h, 1 if on else 0))
+        """Stamp the fused MPNN launches into the clock counters (off by default: measurement only).
+        Libraries from before round 5 (A/B runs) always stamp and lack the switch."""
+        if hasattr(lib(), "pst_set_clock_counters"):
+            self._check(lib().pst_set_clock_counters(self._h, 1 if on else 0))
 
     def clock_counters(self, reset: bool = False) -> np.ndarray:
         """Per fused MPNN layer since the last reset, uint64 [3, 8] (pst_clock_counters): shader
