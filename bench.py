@@ -283,8 +283,10 @@ def wave_slot_occupancy(per_step, slots):
 
 
 def casp14_end_to_end(tk):
-    """SURVEY config 2 as the CLI runs it: parse the 31 CASP14 PDB files (native parser), tokenize
-    from host buffers, write <stem>_tokens.npy. Reported beside `value`."""
+    """SURVEY config 2 as the CLI runs it (InferenceRunner.tokenize's libpst path): read the 31
+    CASP14 PDB files, parse them on the GPU and tokenize (pst_tokenize_pdb_files: the texts go to
+    HBM, the atom37 rows never return to the host), write <stem>_tokens.npy. Reported beside
+    `value`, with the same step through the native host parser for comparison."""
     import tarfile
     import tempfile
     from pst_amd._native import parse_pdb_files, parse_pdb_files_handle
@@ -293,38 +295,59 @@ def casp14_end_to_end(tk):
     if not os.path.exists(arc):
         return None, None
     threads = min(16, host_cores())
-    # inputs and token files on tmpfs where there is one: the figure is the software path (parse,
-    # H2D + tokenize, .npy encode + write syscalls), not the speed of the box's disk
+    # inputs and token files on tmpfs where there is one: the figure is the software path (read,
+    # parse, H2D + tokenize, .npy encode + write syscalls), not the speed of the box's disk
     shm = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
     with tempfile.TemporaryDirectory(dir=shm) as d:
         with tarfile.open(arc) as tf:
             tf.extractall(d, members=[m for m in tf.getmembers() if m.isfile() and m.name.endswith(".pdb")])
         files = sorted(os.path.join(d, "casp14_pdbs", f) for f in os.listdir(os.path.join(d, "casp14_pdbs")))
-        runs = []
-        for rep in range(6):  # first pass warms the page cache and the context's workspace
+        names = [os.path.basename(f)[:-4] + "_tokens" for f in files]
+        runs, host_runs = [], []
+        for rep in range(7):  # first pass warms the page cache and the context's buffers
             out = os.path.join(d, f"out{rep}")
             os.makedirs(out)
             t0 = time.perf_counter()
-            H = parse_pdb_files_handle(files, n_threads=threads)  # Bio's float32 coords, kept in libpst
+            tok, nt, _, off = tk.tokenize_pdb_files(files, n_threads=threads)
             t1 = time.perf_counter()
-            tok, nt, _ = tk.tokenize_pdb_batch(H)  # page-locked staging inside libpst, pst_tokenize_f32
-            off = H.offsets()
+            save_npy_files([os.path.join(out, nm) for nm in names],
+                           [tok[int(off[i]):int(off[i]) + nt[i]].reshape(1, -1) for i in range(len(files))])
+            t2 = time.perf_counter()
+            if rep:
+                runs.append((t2 - t0, t1 - t0, t2 - t1))
+            gpu_files = len(files) - tk.pdb_files_host_parsed()
+            # the same step with the native host parser (pst_pdb_parse_files + pst_tokenize_pdb_batch)
+            hout = os.path.join(d, f"hout{rep}")
+            os.makedirs(hout)
+            t0 = time.perf_counter()
+            H = parse_pdb_files_handle(files, n_threads=threads)
+            t1 = time.perf_counter()
+            htok, hnt, _ = tk.tokenize_pdb_batch(H)
+            hoff = H.offsets()
             H.close()
             t2 = time.perf_counter()
-            save_npy_files([os.path.join(out, os.path.basename(f)[:-4] + "_tokens") for f in files],
-                           [tok[int(off[i]):int(off[i]) + nt[i]].reshape(1, -1) for i in range(len(files))])
+            save_npy_files([os.path.join(hout, nm) for nm in names],
+                           [htok[int(hoff[i]):int(hoff[i]) + hnt[i]].reshape(1, -1) for i in range(len(files))])
             t3 = time.perf_counter()
             if rep:
-                runs.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2))
+                host_runs.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2))
+        assert np.array_equal(off, hoff) and np.array_equal(nt, hnt)
+        same = all(np.array_equal(tok[int(off[i]):int(off[i]) + nt[i]], htok[int(off[i]):int(off[i]) + nt[i]])
+                   for i in range(len(files)))
         B = parse_pdb_files(files, n_threads=threads, float32=True)  # arrays for the CPU baseline
-        assert np.array_equal(B.offsets, off)
         R = int(B.offsets[-1])
-        casp = (B.positions.astype(np.float64), np.array(B.flags), np.array(B.offsets), (tok.copy(), np.array(nt)))
-        tot, parse, tok, write = runs[int(np.argsort([r[0] for r in runs])[len(runs) // 2])]  # median run
+        casp = (B.positions.astype(np.float64), np.array(B.flags), np.array(B.offsets), (htok.copy(), np.array(hnt)))
+        tot, rpt, write = runs[int(np.argsort([r[0] for r in runs])[len(runs) // 2])]  # median run
+        htot, hparse, htokz, hwrite = host_runs[int(np.argsort([r[0] for r in host_runs])[len(host_runs) // 2])]
         res = {"workload": "CASP14 31 structures (SURVEY config 2), codebook 4096, df 1", "residues": R,
-               "parse_ms": round(parse * 1e3, 2), "tokenize_ms": round(tok * 1e3, 2),
-               "write_ms": round(write * 1e3, 2), "residues_per_s": round(R / tot, 1),
-               "parse_threads": threads, "runs": f"median of {len(runs)} after one warm-up",
+               "read_parse_tokenize_ms": round(rpt * 1e3, 2), "write_ms": round(write * 1e3, 2),
+               "residues_per_s": round(R / tot, 1), "files_parsed_on_gpu": gpu_files,
+               "path": "pst_tokenize_pdb_files (files read on the host pool into page-locked memory, text to HBM, "
+                       "parse on the GPU, tokenize) + native token-file writer",
+               "host_parser_path": {"parse_ms": round(hparse * 1e3, 2), "tokenize_ms": round(htokz * 1e3, 2),
+                                    "write_ms": round(hwrite * 1e3, 2), "residues_per_s": round(R / htot, 1),
+                                    "tokens_identical": bool(same)},
+               "threads": threads, "runs": f"median of {len(runs)} after one warm-up",
                "files_on": shm or tempfile.gettempdir()}
     return res, casp
 

@@ -258,6 +258,21 @@ void pst_pdb_batch_free(pst_pdb_batch* b);
  * tokens_out [R] (R from pst_pdb_batch_sizes), n_tokens_out / n_nodes_out [n] (may be NULL). */
 int pst_tokenize_pdb_batch(pst_ctx* ctx, const pst_pdb_batch* b, uint32_t* tokens_out, int32_t* n_tokens_out,
                            int32_t* n_nodes_out);
+/* The CLI's read -> parse -> tokenize step with the parse on the GPU: the n files are read into
+ * page-locked memory on n_threads host threads, their text copied to HBM once, and one workgroup
+ * per file turns it into atom37 rows in the tokenizer's input buffers (pst_pdb_gpu.hip): the
+ * positions never return to the host. Files outside the GPU fast path (MODEL records, altlocs,
+ * insertion codes, unusual columns or bytes, residues that are not contiguous; pst_pdb_gpu.hip)
+ * are parsed by the native host parser instead, with its results and its errors (PST_E_INVALID +
+ * the parser's message). Same rows as pst_pdb_parse_files + pst_tokenize_f32, bit for bit.
+ * tokens_out [tokens_cap] receives R token slots (raw-offset layout, R = offsets_out[n]; a
+ * residue needs >= 55 bytes of file, so sum(file sizes) / 54 + n always suffices),
+ * n_tokens_out / n_nodes_out [n] and offsets_out [n+1] may be NULL. */
+int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, int32_t n_threads,
+                           uint32_t* tokens_out, int64_t tokens_cap, int32_t* n_tokens_out, int32_t* n_nodes_out,
+                           int64_t* offsets_out);
+/* files of the last pst_tokenize_pdb_files call that the host parser took (-1: no context) */
+int32_t pst_pdb_files_host_parsed(const pst_ctx* ctx);
 
 /* Token-file output of the tokenize loop (scripts/inference_runner.py:313-321 writes one
  * np.save per protein): n whole files written (created / truncated) from host buffers on
@@ -290,6 +305,8 @@ void* pst_stream(pst_ctx* ctx);
 /* Debug: copy an intermediate of the LAST call to host.
  *   which = 0..3: node features after init embed / MPNN layer 1..3, [R,128] (raw slot rows)
  *   which = 10:   edge features [R*k, 32] float (27 used), which = 11: senders [R*k] int32
+ *   which = 13:   input positions [R,37,3] float32 of the last float32-input call (pst_tokenize_f32,
+ *                 pst_tokenize_pdb_batch, pst_tokenize_pdb_files), which = 14: its flags [R,37] u8
  *   which = 20:   int32[20] plan of the last pst_tokenize(_f32) call: [0] copy ranges of its first
  *                 chunk (0 = one copy, the range branch not taken), [1] pipeline chunks C,
  *                 [2 .. 2+C] the chunks' first proteins (and n_prot), [11 .. 11+C-1] each chunk's

@@ -11,10 +11,16 @@
 #include <string>
 #include <vector>
 
+#include <sys/stat.h>
+
+#include <atomic>
+
 #include "../../include/pst.h"
 #include "pst_pe.h"
 #include "pst_kernels.h"
 #include "pst_frag.h"
+#include "pst_pool.h"
+#include "pst_residue_tables.h"
 
 namespace {
 using namespace pst_host;
@@ -295,6 +301,15 @@ struct pst_ctx {
   float* h_stage_pos = nullptr;
   uint8_t* h_stage_flags = nullptr;
   int64_t h_stage_cap = 0;
+  // pst_tokenize_pdb_files (grow-only): page-locked file text, device scratch of the GPU parse,
+  // page-locked per-file counts
+  char* h_text = nullptr;
+  size_t h_text_cap = 0;
+  void* d_pdb = nullptr;
+  size_t d_pdb_cap = 0;
+  int32_t* h_pdb_counts = nullptr;
+  int64_t h_pdb_counts_cap = 0;
+  int32_t last_pdb_host_files = 0;  // files of the last pst_tokenize_pdb_files the host parser took
   bool clock_on = false;  // pst_set_clock_counters: stamp the fused MPNN launches (off by default)
 };
 
@@ -948,6 +963,9 @@ int pst_destroy(pst_ctx* ctx) {
   if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
   if (ctx->h_stage_pos) (void)hipHostFree(ctx->h_stage_pos);
   if (ctx->h_stage_flags) (void)hipHostFree(ctx->h_stage_flags);
+  if (ctx->h_text) (void)hipHostFree(ctx->h_text);
+  if (ctx->h_pdb_counts) (void)hipHostFree(ctx->h_pdb_counts);
+  if (ctx->d_pdb) (void)hipFree(ctx->d_pdb);
   for (hipStream_t cs : {ctx->copy_stream, ctx->copy_stream2})
     if (cs) {
       (void)hipStreamSynchronize(cs);
@@ -1221,6 +1239,212 @@ int pst_tokenize_pdb_batch(pst_ctx* ctx, const pst_pdb_batch* b, uint32_t* token
                        n_nodes_out);
 }
 
+int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, int32_t n_threads,
+                           uint32_t* tokens_out, int64_t tokens_cap, int32_t* n_tokens_out, int32_t* n_nodes_out,
+                           int64_t* offsets_out) {
+  if (!ctx) return PST_E_INVALID;
+  ctx->err.clear();
+  if (n <= 0 || !paths || !tokens_out) return fail(ctx, PST_E_INVALID, "empty batch or null buffer");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int threads = std::max(1, n_threads);
+  auto& pool = pst::HostPool::get();
+  // ---- file sizes, then the texts read straight into page-locked memory
+  std::vector<int64_t> fsz(n, 0);
+  std::atomic<int> bad_file(-1);
+  pool.run(n, threads, [&](int i) {
+    struct stat st;
+    if (stat(paths[i], &st) != 0) bad_file.store(i);
+    else fsz[i] = (int64_t)st.st_size;
+  });
+  if (bad_file.load() >= 0) return fail(ctx, PST_E_INVALID, std::string("cannot open ") + paths[bad_file.load()]);
+  std::vector<int64_t> foff(n + 1, 0), rbase(n + 1, 0);
+  for (int i = 0; i < n; ++i) {
+    foff[i + 1] = foff[i] + fsz[i];
+    rbase[i + 1] = rbase[i] + fsz[i] / 54 + 1;  // an ATOM/HETATM record spans >= 54 columns + a separator
+  }
+  const int64_t T = foff[n], RB = rbase[n];
+  if (T + 1 > (int64_t)ctx->h_text_cap) {
+    if (ctx->h_text) (void)hipHostFree(ctx->h_text);
+    ctx->h_text = nullptr;
+    ctx->h_text_cap = 0;
+    const size_t cap = (size_t)std::max<int64_t>(T + 1, 1 << 20);
+    HIPCHK(hipHostMalloc((void**)&ctx->h_text, cap));
+    ctx->h_text_cap = cap;
+  }
+  pool.run(n, threads, [&](int i) {
+    FILE* fh = fopen(paths[i], "rb");
+    if (!fh) {
+      bad_file.store(i);
+      return;
+    }
+    const size_t got = fsz[i] ? fread(ctx->h_text + foff[i], 1, (size_t)fsz[i], fh) : 0;
+    fclose(fh);
+    if ((int64_t)got != fsz[i]) bad_file.store(i);
+  });
+  if (bad_file.load() >= 0) return fail(ctx, PST_E_INVALID, std::string("cannot read ") + paths[bad_file.load()]);
+  // ---- device scratch of the GPU parse (one grow-only allocation)
+  pst::PdbScanArgs a{};
+  {
+    struct Item {
+      void** p;
+      size_t bytes;
+    };
+    const size_t L = (size_t)(T + n);
+    Item items[] = {{(void**)&a.text, (size_t)T + 1},
+                    {(void**)&a.file_off, sizeof(int64_t) * (n + 1)},
+                    {(void**)&a.rec_base, sizeof(int64_t) * (n + 1)},
+                    {(void**)&a.res_off, sizeof(int64_t) * (n + 1)},
+                    {(void**)&a.line_start, sizeof(int32_t) * L},
+                    {(void**)&a.line_kind, L},
+                    {(void**)&a.rec_chain, (size_t)RB},
+                    {(void**)&a.rec_het, (size_t)RB},
+                    {(void**)&a.rec_atom, (size_t)RB},
+                    {(void**)&a.rec_resseq, sizeof(int32_t) * RB},
+                    {(void**)&a.rec_name, sizeof(uint32_t) * RB},
+                    {(void**)&a.rec_xyz, sizeof(float) * 3 * RB},
+                    {(void**)&a.rec_run, sizeof(int32_t) * RB},
+                    {(void**)&a.run_first, sizeof(int32_t) * RB},
+                    {(void**)&a.run_out, sizeof(int32_t) * RB},
+                    {(void**)&a.slot, sizeof(int32_t) * 37 * RB},
+                    {(void**)&a.n_res, sizeof(int32_t) * 3 * n}};
+    size_t total = 0;
+    for (const auto& it : items) total += (it.bytes + 255) / 256 * 256;
+    if (total > ctx->d_pdb_cap) {
+      if (ctx->d_pdb) (void)hipFree(ctx->d_pdb);
+      ctx->d_pdb = nullptr;
+      ctx->d_pdb_cap = 0;
+      hipError_t e = hipMalloc(&ctx->d_pdb, total);
+      if (e != hipSuccess) return fail(ctx, PST_E_NOMEM, std::string("PDB parse scratch: ") + hipGetErrorString(e));
+      ctx->d_pdb_cap = total;
+    }
+    char* q = (char*)ctx->d_pdb;
+    for (const auto& it : items) {
+      *it.p = q;
+      q += (it.bytes + 255) / 256 * 256;
+    }
+    a.n_run = a.n_res + n;
+    a.host_path = a.n_res + 2 * n;
+  }
+  if (3 * (int64_t)n > ctx->h_pdb_counts_cap) {
+    if (ctx->h_pdb_counts) (void)hipHostFree(ctx->h_pdb_counts);
+    ctx->h_pdb_counts = nullptr;
+    ctx->h_pdb_counts_cap = 0;
+    HIPCHK(hipHostMalloc((void**)&ctx->h_pdb_counts, sizeof(int32_t) * 3 * std::max(n, 64)));
+    ctx->h_pdb_counts_cap = 3 * std::max(n, 64);
+  }
+  for (int q = 0; q < 37; ++q) {
+    const char* nm = pst::kAtomNames[q];
+    uint32_t k = 0;
+    std::memcpy(&k, nm, std::min<size_t>(4, strlen(nm)));
+    a.tab.atom_key[q] = k;
+  }
+  for (int r = 0; r < 20; ++r) {
+    uint32_t k = 0;
+    std::memcpy(&k, pst::kResName3[r], 3);
+    a.tab.res_key[r] = k;
+  }
+  std::memcpy(&a.tab.hoh, "HOH\0", 4);
+  std::memcpy(&a.tab.wat, "WAT\0", 4);
+  for (int r = 0; r < 21; ++r)
+    for (int q = 0; q < 37; ++q) a.tab.exists[r][q] = pst::kResAtomExists[r][q];
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync((void*)a.text, ctx->h_text, (size_t)T, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync((void*)a.file_off, foff.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync((void*)a.rec_base, rbase.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+  pst::launch_pdb_scan(a, n, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ctx->h_pdb_counts, a.n_res, sizeof(int32_t) * 3 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const int32_t* g_res = ctx->h_pdb_counts;
+  const int32_t* g_host = ctx->h_pdb_counts + 2 * n;
+  // ---- the files outside the fast path: the native host parser (its results and its errors)
+  std::vector<int32_t> host_ids;
+  for (int i = 0; i < n; ++i)
+    if (g_host[i]) host_ids.push_back(i);
+  pst_pdb_batch* hb = nullptr;
+  std::vector<int64_t> hoff(host_ids.size() + 1, 0);
+  struct BatchFree {
+    pst_pdb_batch** b;
+    ~BatchFree() {
+      if (*b) pst_pdb_batch_free(*b);
+    }
+  } hb_free{&hb};
+  if (!host_ids.empty()) {
+    std::vector<const char*> tp;
+    std::vector<size_t> tl;
+    for (int i : host_ids) {
+      tp.push_back(ctx->h_text + foff[i]);
+      tl.push_back((size_t)fsz[i]);
+    }
+    pst_pdb_parse_strings(tp.data(), tl.data(), (int32_t)host_ids.size(), 0, threads, &hb);
+    std::vector<int32_t> hst(host_ids.size());
+    pst_pdb_batch_copy_f32(hb, nullptr, nullptr, nullptr, hoff.data(), hst.data());
+    for (size_t j = 0; j < host_ids.size(); ++j)
+      if (hst[j] != PST_OK) return fail(ctx, PST_E_INVALID, pst_pdb_batch_error(hb, (int32_t)j));
+  }
+  std::vector<int64_t> off(n + 1, 0);
+  {
+    size_t j = 0;
+    for (int i = 0; i < n; ++i) {
+      const int64_t ri = g_host[i] ? hoff[j + 1] - hoff[j] : g_res[i];
+      if (g_host[i]) ++j;
+      off[i + 1] = off[i] + ri;
+    }
+  }
+  int rc = validate(ctx, off.data(), n);
+  if (rc) return rc;
+  const int64_t R = off[n];
+  if (R > tokens_cap) return fail(ctx, PST_E_INVALID, "token buffer too small");
+  rc = ensure_workspace(ctx, R, n);
+  if (rc) return rc;
+  auto& w = ctx->w;
+  a.pos = reinterpret_cast<float*>(w.pos);
+  a.flags = w.flags;
+  HIPCHK(hipMemcpyAsync((void*)a.res_off, off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+  pst::launch_pdb_write(a, n, st);
+  HIPCHK(hipGetLastError());
+  if (!host_ids.empty()) {  // host-parsed rows into their places (through the page-locked staging)
+    const int64_t HR = hoff.back();
+    if (HR > ctx->h_stage_cap) {
+      if (ctx->h_stage_pos) (void)hipHostFree(ctx->h_stage_pos);
+      if (ctx->h_stage_flags) (void)hipHostFree(ctx->h_stage_flags);
+      ctx->h_stage_pos = nullptr;
+      ctx->h_stage_flags = nullptr;
+      ctx->h_stage_cap = 0;
+      const int64_t cap = std::max<int64_t>(HR, 4096);
+      HIPCHK(hipHostMalloc((void**)&ctx->h_stage_pos, sizeof(float) * 111 * cap));
+      HIPCHK(hipHostMalloc((void**)&ctx->h_stage_flags, 37 * cap));
+      ctx->h_stage_cap = cap;
+    }
+    pst_pdb_batch_copy_f32(hb, ctx->h_stage_pos, ctx->h_stage_flags, nullptr, nullptr, nullptr);
+    for (size_t j = 0; j < host_ids.size(); ++j) {
+      const int64_t r0 = off[host_ids[j]], nr = hoff[j + 1] - hoff[j];
+      if (!nr) continue;
+      HIPCHK(hipMemcpyAsync(a.pos + 111 * r0, ctx->h_stage_pos + 111 * hoff[j], sizeof(float) * 111 * nr,
+                            hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(w.flags + 37 * r0, ctx->h_stage_flags + 37 * hoff[j], 37 * nr, hipMemcpyHostToDevice, st));
+    }
+  }
+  ctx->last_pdb_host_files = (int32_t)host_ids.size();
+  rc = run(ctx, nullptr, w.flags, off.data(), n, w.tokens, w.n_tok, w.n_nodes, false, 0, a.pos);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_ntok, dim3((n + 255) / 256), dim3(256), 0, st, w.n_nodes, w.n_tok, n, ctx->df);
+  HIPCHK(hipMemcpyAsync(tokens_out, w.tokens, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, st));
+  if ((n_tokens_out || n_nodes_out) && ctx->h_counts) {
+    HIPCHK(hipMemcpyAsync(ctx->h_counts, w.n_tok, sizeof(int32_t) * (ctx->cap_B + n), hipMemcpyDeviceToHost, st));
+  } else {
+    if (n_tokens_out) HIPCHK(hipMemcpyAsync(n_tokens_out, w.n_tok, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+    if (n_nodes_out) HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (n_tokens_out && ctx->h_counts) std::memcpy(n_tokens_out, ctx->h_counts, sizeof(int32_t) * n);
+  if (n_nodes_out && ctx->h_counts) std::memcpy(n_nodes_out, ctx->h_counts + ctx->cap_B, sizeof(int32_t) * n);
+  if (offsets_out) std::memcpy(offsets_out, off.data(), sizeof(int64_t) * (n + 1));
+  return PST_OK;
+}
+
+int32_t pst_pdb_files_host_parsed(const pst_ctx* ctx) { return ctx ? ctx->last_pdb_host_files : -1; }
+
 int pst_build_graph(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_flags, const int64_t* offsets,
                     int32_t n_prot, int32_t* senders_out, float* edge_features_out, double* ca_out,
                     int32_t* n_nodes_out) {
@@ -1438,6 +1662,10 @@ int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes) {
     for (size_t e = 0; e < (size_t)ctx->last_R * KNN; ++e)
       for (int f = 0; f < 32; ++f) o[e * 32 + f] = f < pst::FEAT_USED ? tmp[e * 32 + pst::feat_slot(f)] : 0.0f;
     return PST_OK;
+  } else if (which == 13 || which == 14) {  // the last call's input rows: positions f32 (pst_tokenize_f32 /
+    // pst_tokenize_pdb_batch / pst_tokenize_pdb_files) [R,37,3], flags [R,37]
+    need = (size_t)ctx->last_R * (which == 13 ? 111 * sizeof(float) : 37);
+    src = which == 13 ? (const void*)ctx->w.pos : (const void*)ctx->w.flags;
   } else if (which == 11) {
     src = ctx->w.senders;
     need = (size_t)ctx->last_R * KNN * sizeof(int32_t);

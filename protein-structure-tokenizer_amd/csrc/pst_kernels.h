@@ -176,6 +176,41 @@ struct FsqAuxArgs {
   uint32_t* hist;      // [K] (zeroed by the caller) or null
 };
 
+// PDB text -> atom37 rows on the GPU (pst_pdb_gpu.hip, pst_tokenize_pdb_files)
+struct PdbTables {
+  uint32_t atom_key[37];  // atom37 names packed little-endian (stripped, <= 4 characters)
+  uint32_t res_key[20];   // the 20 standard residue names, packed
+  uint32_t hoh, wat;
+  uint8_t exists[21][37];  // residue type x atom37: the atom belongs to the residue (UNK: none)
+};
+struct PdbScanArgs {
+  const char* text;          // all files back to back
+  const int64_t* file_off;   // [n+1] byte offsets
+  const int64_t* rec_base;   // [n+1] record / residue-run scratch base per file (>= len/54 + 1 each)
+  int32_t* line_start;       // [total bytes + n] line starts, file f from file_off[f] + f
+  uint8_t* line_kind;        // same indexing
+  // records (ATOM / HETATM lines), file f from rec_base[f]
+  uint8_t* rec_chain;
+  uint8_t* rec_het;          // 0 ATOM, 1 water, 2 other HETATM
+  int8_t* rec_atom;          // atom37 index or -1
+  int32_t* rec_resseq;
+  uint32_t* rec_name;        // residue name, packed
+  float* rec_xyz;            // [records][3]
+  int32_t* rec_run;          // residue run of the record
+  int32_t* run_first;        // first record of each run
+  int32_t* run_out;          // kept-residue ordinal of each run (-1: no atom37 atom)
+  int32_t* slot;             // [runs][37] first record of each atom37 name
+  int32_t* n_res;            // [n] kept residues
+  int32_t* n_run;            // [n]
+  int32_t* host_path;        // [n] 1 = outside the fast path: parsed on the host instead
+  const int64_t* res_off;    // [n+1] output row of each file's first residue (k_pdb_write)
+  float* pos;                // [R,37,3] float32 positions (the tokenizer's input)
+  uint8_t* flags;            // [R,37]
+  PdbTables tab;
+};
+void launch_pdb_scan(const PdbScanArgs& a, int n_files, hipStream_t st);
+void launch_pdb_write(const PdbScanArgs& a, int n_files, hipStream_t st);
+
 void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st);
 void launch_knn(const KnnArgs& a, hipStream_t st);
 // node_coop (split schedule only): node update as k_mpnn_node_coop, four waves per 32 receivers

@@ -1,0 +1,342 @@
+// pst_pdb_gpu.hip — PDB text → atom37 rows on the GPU: the parse half of pst_tokenize_pdb_files.
+//
+// The host reads the files into one page-locked buffer and copies the text to HBM (3.9 MB for
+// the 31 CASP14 structures); one workgroup per file then does what the native parser's two
+// passes do (pst_pdb.cpp, the restatement of Bio's PDBParser in pst_amd/pdb.py), and a second
+// launch writes each kept residue's atom37 row straight into the tokenizer's input buffers —
+// the positions never travel back to the host. The fast path covers the files PDB writers
+// emit; anything else is flagged per file and parsed by the native host parser instead, so the
+// product's semantics stay those of pst_pdb.cpp file for file:
+//   * bytes: printable ASCII, '\n' and '\r' (a '\r' ends a line, as in pst_pdb.cpp; the empty
+//     line between "\r\n" is not a record) — a tab or any other byte: host path;
+//   * records: the header ends at the first ATOM / HETATM / MODEL line, the coordinates at the
+//     first "END   " / "CONECT" line after it; a MODEL or ENDMDL record in between: host path
+//     (single-model files with MODEL lines, and every multi-model error, stay there);
+//   * ATOM / HETATM: at least 54 columns, altloc and insertion code blank, resseq an integer,
+//     x / y / z in the fixed "%8.3f" form (m / 1000.0 as one IEEE division: the double strtod
+//     gives, then rounded to float32 as Bio stores atom.coord), occupancy blank or decimal;
+//     anything else: host path (which parses it or raises the reference's error);
+//   * residues: keyed by (chain, het flag, resseq, resname when the het flag is "H_<resname>"),
+//     contiguous in the file: each chain one block of lines, and within a chain the keys strictly
+//     increasing in (ATOM before HETATM, resseq) — so a residue never reappears and Bio's
+//     order of first appearance is the file order; otherwise: host path;
+//   * atoms: the first record of an atom37 name in its residue (no altlocs on this path); names
+//     outside atom37 are dropped; residues without an atom37 atom are skipped; the residue type
+//     is the first record's resname among the 20 standard ones, else UNK.
+// Every choice above is checked against the host parser bit for bit on the GPU
+// (tests/test_gpu_cli.py: positions and flags of every CASP14 file and of handcrafted files
+// covering each host-path trigger).
+#include "pst_kernels.h"
+
+namespace pst {
+
+namespace {
+
+constexpr int PDB_THREADS = 1024;
+constexpr int PDB_INT_MAX = 0x7fffffff;
+
+enum : uint8_t { K_OTHER = 0, K_ATOM = 1, K_HETATM = 2, K_MODEL = 3, K_ENDMDL = 4, K_STOP = 5 };
+
+// exclusive prefix sum over the workgroup (PDB_THREADS threads); *total = the sum
+__device__ int block_scan(int v, int* total) {
+  __shared__ int wsum[PDB_THREADS / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int i = 0; i < PDB_THREADS / 64; ++i) {
+    const int s = wsum[i];
+    if (i < w) base += s;
+    tot += s;
+  }
+  __syncthreads();  // wsum is reused by the next call
+  *total = tot;
+  return base + x - v;
+}
+
+__device__ __forceinline__ bool is6(const char* p, const char* s) {
+  return p[0] == s[0] && p[1] == s[1] && p[2] == s[2] && p[3] == s[3] && p[4] == s[4] && p[5] == s[5];
+}
+
+// stripped field [a, b) of a line of length ll (spaces only: tabs never reach this path)
+__device__ __forceinline__ void field(const char* line, int ll, int a, int b, int* s, int* n) {
+  if (b > ll) b = ll;
+  while (a < b && line[a] == ' ') ++a;
+  while (b > a && line[b - 1] == ' ') --b;
+  *s = a;
+  *n = b > a ? b - a : 0;
+}
+
+__device__ __forceinline__ uint32_t pack4(const char* p, int n) {
+  uint32_t k = 0;
+  for (int i = 0; i < n && i < 4; ++i) k |= (uint32_t)(uint8_t)p[i] << (8 * i);
+  return k;
+}
+
+// "%8.3f" field at column a (pst_pdb.cpp coord_fixed): false = not that form
+__device__ __forceinline__ bool coord_fixed(const char* p, double* v) {
+  if (p[4] != '.') return false;
+  const unsigned d5 = (unsigned)(p[5] - '0'), d6 = (unsigned)(p[6] - '0'), d7 = (unsigned)(p[7] - '0');
+  if (d5 > 9 || d6 > 9 || d7 > 9) return false;
+  int i = 0;
+  while (i < 4 && p[i] == ' ') ++i;
+  bool neg = false;
+  if (i < 4 && (p[i] == '-' || p[i] == '+')) {
+    neg = p[i] == '-';
+    ++i;
+  }
+  if (i == 4) return false;
+  int64_t m = 0;
+  for (; i < 4; ++i) {
+    const unsigned d = (unsigned)(p[i] - '0');
+    if (d > 9) return false;
+    m = m * 10 + d;
+  }
+  m = (m * 10 + d5) * 100 + d6 * 10 + d7;
+  const double r = (double)m / 1000.0;
+  *v = neg ? -r : r;
+  return true;
+}
+
+__device__ __forceinline__ int line_end(const PdbScanArgs& a, int64_t lb, int i, int n_lines, int len) {
+  return i + 1 < n_lines ? a.line_start[lb + i + 1] - 1 : len;
+}
+
+}  // namespace
+
+// One workgroup per file: lines, records, residues, atom slots; per-file kept-residue counts and
+// the host-path flag. Scratch per file f: lines at line_base = file_off[f] + f, records and
+// residue runs at rec_base[f] (rec_base[f+1] - rec_base[f] >= len / 54 + 1 records fit).
+__global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int64_t f0 = a.file_off[f];
+  const int len = (int)(a.file_off[f + 1] - f0);
+  const char* tx = a.text + f0;
+  const int64_t lb = f0 + f, rb = a.rec_base[f];
+  const int rec_cap = (int)(a.rec_base[f + 1] - rb);
+  __shared__ int s_bad, s_start, s_stop, s_chain_seg[256];
+  if (tid == 0) {
+    s_bad = 0;
+    s_start = PDB_INT_MAX;
+    s_stop = PDB_INT_MAX;
+  }
+  for (int c = tid; c < 256; c += PDB_THREADS) s_chain_seg[c] = 0;
+  __syncthreads();
+  // ---- lines: separators '\n' and '\r' counted per contiguous chunk, then their positions
+  const int chunk = (len + PDB_THREADS - 1) / PDB_THREADS;
+  const int c0 = min(len, tid * chunk), c1 = min(len, c0 + chunk);
+  int cnt = 0;
+  bool bad = false;
+  for (int i = c0; i < c1; ++i) {
+    const char c = tx[i];
+    if (c == '\n' || c == '\r') ++cnt;
+    else if (c < 0x20 || c > 0x7e) bad = true;
+  }
+  if (bad) s_bad = 1;
+  int n_sep = 0;
+  int at = block_scan(cnt, &n_sep) + 1;
+  if (tid == 0) a.line_start[lb] = 0;
+  for (int i = c0; i < c1; ++i) {
+    const char c = tx[i];
+    if (c == '\n' || c == '\r') a.line_start[lb + at++] = i + 1;
+  }
+  const int n_lines = n_sep + 1;  // the last line may be empty
+  __syncthreads();
+  // ---- record kinds; the header ends at the first ATOM / HETATM / MODEL line
+  for (int i = tid; i < n_lines; i += PDB_THREADS) {
+    const int s = a.line_start[lb + i], ll = line_end(a, lb, i, n_lines, len) - s;
+    uint8_t k = K_OTHER;
+    if (ll >= 6) {
+      const char* p = tx + s;
+      if (is6(p, "ATOM  ")) k = K_ATOM;
+      else if (is6(p, "HETATM")) k = K_HETATM;
+      else if (is6(p, "MODEL ")) k = K_MODEL;
+      else if (is6(p, "ENDMDL")) k = K_ENDMDL;
+      else if (is6(p, "END   ") || is6(p, "CONECT")) k = K_STOP;
+    }
+    a.line_kind[lb + i] = k;
+    if (k == K_ATOM || k == K_HETATM || k == K_MODEL) atomicMin(&s_start, i);
+  }
+  __syncthreads();
+  const int start = s_start;
+  for (int i = tid; i < n_lines; i += PDB_THREADS)
+    if (i > start && a.line_kind[lb + i] == K_STOP) atomicMin(&s_stop, i);
+  __syncthreads();
+  const int stop = min(s_stop, n_lines);
+  // ---- ATOM / HETATM records of [start, stop) in line order, fields parsed
+  int n_rec = 0;
+  for (int t0 = start; t0 < stop; t0 += PDB_THREADS) {
+    const int i = t0 + tid;
+    const uint8_t k = i < stop ? a.line_kind[lb + i] : K_OTHER;
+    if (k == K_MODEL || k == K_ENDMDL) s_bad = 1;
+    const bool rec = k == K_ATOM || k == K_HETATM;
+    int tile = 0;
+    const int r = n_rec + block_scan(rec ? 1 : 0, &tile);
+    n_rec += tile;
+    if (!rec) continue;
+    if (r >= rec_cap) {  // cannot happen for >= 54-column records; guards the scratch bounds
+      s_bad = 1;
+      continue;
+    }
+    const int s = a.line_start[lb + i], ll = line_end(a, lb, i, n_lines, len) - s;
+    const char* L = tx + s;
+    bool ok = ll >= 54 && L[16] == ' ' && L[26] == ' ';
+    double x = 0.0, y = 0.0, z = 0.0;
+    int rs = 0;
+    if (ok) ok = coord_fixed(L + 30, &x) && coord_fixed(L + 38, &y) && coord_fixed(L + 46, &z);
+    if (ok) {  // resseq: optional sign, 1-4 digits
+      int fs, fn;
+      field(L, ll, 22, 26, &fs, &fn);
+      int j = fs, sg = 1;
+      if (fn > 0 && (L[j] == '-' || L[j] == '+')) {
+        sg = L[j] == '-' ? -1 : 1;
+        ++j;
+      }
+      ok = j < fs + fn;
+      for (; ok && j < fs + fn; ++j) {
+        const unsigned d = (unsigned)(L[j] - '0');
+        if (d > 9) ok = false;
+        rs = rs * 10 + (int)d;
+      }
+      rs *= sg;
+    }
+    if (ok && ll > 54) {  // occupancy blank or [sign] digits [. digits]
+      int fs, fn;
+      field(L, ll, 54, 60, &fs, &fn);
+      int j = fs, digits = 0, dots = 0;
+      if (fn > 0 && (L[j] == '-' || L[j] == '+')) ++j;
+      for (; ok && j < fs + fn; ++j) {
+        if (L[j] >= '0' && L[j] <= '9') ++digits;
+        else if (L[j] == '.' && dots == 0) ++dots;
+        else ok = false;
+      }
+      if (fn > 0 && digits == 0) ok = false;
+    }
+    if (!ok) {
+      s_bad = 1;
+      continue;
+    }
+    int ns, nn, rsn, rsl;
+    field(L, ll, 12, 16, &ns, &nn);
+    field(L, ll, 17, 20, &rsn, &rsl);
+    const uint32_t name = pack4(L + ns, nn), resname = pack4(L + rsn, rsl);
+    int atom = -1;
+    if (nn >= 1 && nn <= 4)
+      for (int q = 0; q < 37; ++q)
+        if (a.tab.atom_key[q] == name) atom = q;
+    const bool water = rsl == 3 && (resname == a.tab.hoh || resname == a.tab.wat);
+    const int64_t o = rb + r;
+    a.rec_chain[o] = (uint8_t)L[21];
+    a.rec_het[o] = k == K_ATOM ? 0 : water ? 1 : 2;
+    a.rec_atom[o] = (int8_t)atom;
+    a.rec_resseq[o] = rs;
+    a.rec_name[o] = rsl <= 4 ? resname : 0xffffffffu;  // a 4+ character name is never standard
+    a.rec_xyz[3 * o + 0] = (float)x;
+    a.rec_xyz[3 * o + 1] = (float)y;
+    a.rec_xyz[3 * o + 2] = (float)z;
+  }
+  __syncthreads();
+  n_rec = min(n_rec, rec_cap);
+  // ---- residue runs: a record opens one when its key differs from the previous record's
+  auto same = [&](int64_t p, int64_t q) {
+    return a.rec_chain[p] == a.rec_chain[q] && a.rec_het[p] == a.rec_het[q] && a.rec_resseq[p] == a.rec_resseq[q] &&
+           (a.rec_het[p] != 2 || a.rec_name[p] == a.rec_name[q]);
+  };
+  int n_run = 0;
+  for (int t0 = 0; t0 < n_rec; t0 += PDB_THREADS) {
+    const int k = t0 + tid;
+    const bool opens = k < n_rec && (k == 0 || !same(rb + k, rb + k - 1));
+    int tile = 0;
+    const int r = n_run + block_scan(opens ? 1 : 0, &tile);
+    if (opens) a.run_first[rb + r] = k;
+    n_run += tile;
+  }
+  __syncthreads();
+  // run of each record (the last run opened at or before it), and the contiguity checks
+  for (int r = tid; r < n_run; r += PDB_THREADS) {
+    const int k0 = a.run_first[rb + r], k1 = r + 1 < n_run ? a.run_first[rb + r + 1] : n_rec;
+    for (int k = k0; k < k1; ++k) a.rec_run[rb + k] = r;
+    const uint8_t ch = a.rec_chain[rb + k0];
+    if (r == 0 || a.rec_chain[rb + a.run_first[rb + r - 1]] != ch) {
+      atomicAdd(&s_chain_seg[ch], 1);
+    } else {  // same chain: keys strictly increasing in (ATOM before HETATM, resseq)
+      const int64_t p = rb + a.run_first[rb + r - 1], q = rb + k0;
+      const int hp = a.rec_het[p] ? 1 : 0, hq = a.rec_het[q] ? 1 : 0;
+      if (!(hq > hp || (hq == hp && a.rec_resseq[q] > a.rec_resseq[p]))) s_bad = 1;
+    }
+  }
+  for (int r = tid; r < n_run * 37; r += PDB_THREADS) a.slot[37 * rb + r] = PDB_INT_MAX;
+  __syncthreads();
+  for (int c = tid; c < 256; c += PDB_THREADS)
+    if (s_chain_seg[c] > 1) s_bad = 1;  // a chain that reappears after another one
+  // ---- atom slots: the first record of each atom37 name in its residue
+  for (int k = tid; k < n_rec; k += PDB_THREADS) {
+    const int at = a.rec_atom[rb + k];
+    if (at >= 0) atomicMin(&a.slot[37 * (rb + a.rec_run[rb + k]) + at], k);
+  }
+  __syncthreads();
+  // ---- kept residues (at least one atom37 atom), numbered in file order
+  int n_keep = 0;
+  for (int t0 = 0; t0 < n_run; t0 += PDB_THREADS) {
+    const int r = t0 + tid;
+    bool keep = false;
+    if (r < n_run)
+      for (int q = 0; q < 37 && !keep; ++q) keep = a.slot[37 * (rb + r) + q] != PDB_INT_MAX;
+    int tile = 0;
+    const int o = n_keep + block_scan(keep ? 1 : 0, &tile);
+    if (r < n_run) a.run_out[rb + r] = keep ? o : -1;
+    n_keep += tile;
+  }
+  if (tid == 0) {
+    a.n_res[f] = n_keep;
+    a.n_run[f] = n_run;
+    a.host_path[f] = s_bad;
+  }
+}
+
+// Kept residue rows of the fast-path files into the tokenizer's inputs: positions float32
+// [R,37,3] (absent atoms 0) and flags [R,37] (bit0 present, bit1 atom37 atom of the residue type).
+__global__ __launch_bounds__(256) void k_pdb_write(PdbScanArgs a) {
+  const int f = blockIdx.x;
+  if (a.host_path[f]) return;
+  const int64_t rb = a.rec_base[f], row0 = a.res_off[f];
+  const int n_run = a.n_run[f];
+  for (int e = threadIdx.x; e < n_run * 37; e += 256) {
+    const int r = e / 37, at = e - 37 * r;
+    const int o = a.run_out[rb + r];
+    if (o < 0) continue;
+    const uint32_t rn = a.rec_name[rb + a.run_first[rb + r]];
+    int rt = 20;
+    for (int q = 0; q < 20; ++q)
+      if (a.tab.res_key[q] == rn) rt = q;
+    const int k = a.slot[37 * (rb + r) + at];
+    const int64_t row = row0 + o;
+    float* p = a.pos + (row * 37 + at) * 3;
+    if (k != PDB_INT_MAX) {
+      p[0] = a.rec_xyz[3 * (rb + k) + 0];
+      p[1] = a.rec_xyz[3 * (rb + k) + 1];
+      p[2] = a.rec_xyz[3 * (rb + k) + 2];
+    } else {
+      p[0] = 0.0f;
+      p[1] = 0.0f;
+      p[2] = 0.0f;
+    }
+    a.flags[row * 37 + at] = (uint8_t)((k != PDB_INT_MAX ? 1 : 0) | (a.tab.exists[rt][at] << 1));
+  }
+}
+
+void launch_pdb_scan(const PdbScanArgs& a, int n_files, hipStream_t st) {
+  hipLaunchKernelGGL(k_pdb_scan, dim3(n_files), dim3(PDB_THREADS), 0, st, a);
+}
+
+void launch_pdb_write(const PdbScanArgs& a, int n_files, hipStream_t st) {
+  hipLaunchKernelGGL(k_pdb_write, dim3(n_files), dim3(256), 0, st, a);
+}
+
+}  // namespace pst

@@ -41,7 +41,8 @@ EXPORTS = ("pst_param_count", "pst_create", "pst_destroy", "pst_last_error", "ps
            "pst_decoder_param_count", "pst_decoder_create", "pst_decoder_destroy", "pst_decoder_last_error",
            "pst_decoder_create_error", "pst_decoder_decode", "pst_decoder_decode_ex", "pst_decoder_debug",
            "pst_build_graph", "pst_clock_counters", "pst_set_clock_counters", "pst_pdb_batch_copy_f32",
-           "pst_decoder_set_timing", "pst_decoder_get_timing", "pst_tokenize_pdb_batch")
+           "pst_decoder_set_timing", "pst_decoder_get_timing", "pst_tokenize_pdb_batch",
+           "pst_tokenize_pdb_files", "pst_pdb_files_host_parsed")
 STAGES = ("prep", "knn", "mpnn0", "mpnn1", "mpnn2", "down")
 
 
@@ -94,7 +95,9 @@ def lib():
         # tests/test_abi.py requires every EXPORTS symbol of the in-tree build
         for name, at in (("pst_set_clock_counters", [P, ctypes.c_int32]),
                          ("pst_decoder_set_timing", [P, ctypes.c_int32]), ("pst_decoder_get_timing", [P, P]),
-                         ("pst_tokenize_pdb_batch", [P, P, P, P, P])):
+                         ("pst_tokenize_pdb_batch", [P, P, P, P, P]),
+                         ("pst_tokenize_pdb_files", [P, P, ctypes.c_int32, ctypes.c_int32, P, ctypes.c_int64, P, P, P]),
+                         ("pst_pdb_files_host_parsed", [P])):
             if hasattr(L, name):
                 getattr(L, name).argtypes = at
         L.pst_pdb_parse_files.argtypes = [P, ctypes.c_int32, ctypes.c_char, ctypes.c_int32, ctypes.POINTER(P)]
@@ -342,6 +345,28 @@ class Tokenizer:
         self._check(lib().pst_tokenize_pdb_batch(self._h, batch._h, _ptr(tok), _ptr(nt), _ptr(nn)))
         return tok, nt, nn
 
+    def tokenize_pdb_files(self, paths: Sequence[str], n_threads: int = 16):
+        """PDB files → (tokens [R] uint32 raw-offset layout, n_tokens [n], n_nodes [n], offsets
+        [n+1]) through pst_tokenize_pdb_files: the texts parsed on the GPU straight into the
+        tokenizer's inputs (files outside the GPU fast path through the native host parser)."""
+        enc = [os.fsencode(p) for p in paths]
+        n = len(enc)
+        arr = (ctypes.c_char_p * max(n, 1))(*enc)
+        cap = sum(os.path.getsize(p) for p in paths) // 54 + n + 1
+        tok = np.empty(cap, np.uint32)
+        nt = np.empty(n, np.int32)
+        nn = np.empty(n, np.int32)
+        off = np.zeros(n + 1, np.int64)
+        self._check(lib().pst_tokenize_pdb_files(self._h, arr, n, n_threads, _ptr(tok), cap, _ptr(nt), _ptr(nn),
+                                                 _ptr(off)))
+        return tok[:int(off[-1])], nt, nn, off
+
+    def pdb_files_host_parsed(self) -> int:
+        """Files of the last tokenize_pdb_files call that took the host parser."""
+        L = lib()
+        L.pst_pdb_files_host_parsed.restype = ctypes.c_int32
+        return int(L.pst_pdb_files_host_parsed(self._h))
+
     def tokenize(self, samples) -> List[np.ndarray]:
         pos, flags, off = pack_samples(samples)
         tok, nt, _ = self.tokenize_packed(pos, flags, off)
@@ -428,6 +453,10 @@ class Tokenizer:
             out = np.zeros(R * 50, np.int32)
         elif which == 12:
             out = np.zeros(R, np.int32)
+        elif which == 13:
+            out = np.zeros((R, 37, 3), np.float32)
+        elif which == 14:
+            out = np.zeros((R, 37), np.uint8)
         else:
             raise ValueError(which)
         self._check(lib().pst_debug_fetch(self._h, which, _ptr(out), out.nbytes))

@@ -199,6 +199,34 @@ class TokenizeFn:
             self._ctx[key] = ent
         return ent[1]
 
+    def tokenize_files(self, model_params: ReplicatedParams, files: Sequence[str], batch_dims: Sequence[int],
+                       n_threads: int = 16) -> Dict[str, np.ndarray]:
+        """The same outputs as `__call__` on the batch collated from `files` (shard i = files
+        i·bs .. i·bs+bs-1 on devices[i]), with the parse on the GPU (pst_tokenize_pdb_files:
+        the texts go to HBM, atom37 rows never return to the host). Raises the libpst error of a
+        bad file (its message, not necessarily the reference's: InferenceRunner.tokenize then
+        re-runs the batch through the reference-shaped path, which raises the reference's)."""
+        n_dev, bs = batch_dims[0], int(np.prod(batch_dims[1:]))
+        if n_dev > len(self.devices):
+            raise ValueError(f"batch has {n_dev} device shards but only {len(self.devices)} devices")
+        out_len = self.cfg.seq_max_size // self.cfg.downsampling_ratio
+        pad = pad_token_value(self.cfg.levels)
+
+        def run(i):
+            t = self._context(model_params, self.devices[i])
+            if not hasattr(t, "tokenize_pdb_files"):  # a stand-in context (CPU tests): the collated path
+                raise _native.PstError("context without pst_tokenize_pdb_files")
+            tok, nt, nn, off = t.tokenize_pdb_files(list(files[i * bs:(i + 1) * bs]), n_threads=n_threads)
+            rows = np.full((bs, out_len), pad, np.uint32)
+            for b in range(bs):
+                rows[b, :nt[b]] = tok[off[b]:off[b] + nt[b]]
+            return rows, nt, nn
+
+        res = list(self._pool.map(run, range(n_dev)))
+        return {"tokens": np.stack([r[0] for r in res]).reshape(*batch_dims, out_len),
+                "n_tokens": np.stack([r[1] for r in res]).reshape(*batch_dims),
+                "n_nodes": np.stack([np.asarray(r[2], np.int32) for r in res]).reshape(*batch_dims)}
+
     def __call__(self, model_params: ReplicatedParams, random_key: Any, batched_graph: ProteinBatch) -> Dict[str, np.ndarray]:
         n_dev = batched_graph.batch_dims[0]
         if n_dev > len(self.devices):
@@ -401,14 +429,38 @@ class InferenceRunner:
                                           sample=parsed.sample(i)) for i, f in enumerate(files)]
             return files, batch_collate([num_device, batch_size_per_device], graphs)
 
+        # libpst's tokenize fn reads, parses and tokenizes each batch with the parse on the GPU
+        # (TokenizeFn.tokenize_files); a batch holding a file that fails there (a size gate, a parse
+        # error, no residue with a full backbone) is re-run through the reference-shaped path below,
+        # which raises the reference's exception for it
+        gpu_parse = isinstance(quantize, TokenizeFn) and not quantize.emit_aux
+
+        def gpu_batch(it):
+            files = pdbs[it * effective_batch_size:(it + 1) * effective_batch_size]
+            for f in files:
+                if not os.path.exists(f):
+                    raise FileNotFoundError(f)
+            try:
+                out = quantize.tokenize_files(model_params, files, [num_device, batch_size_per_device],
+                                              n_threads=PARSE_THREADS)
+            except (ValueError, NotImplementedError, _native.PstError):
+                return files, None
+            return (files, out) if bool(np.all(out["n_nodes"] > 0)) else (files, None)
+
         with _cf.ThreadPoolExecutor(max_workers=1) as io:
-            nxt = io.submit(load, 0) if num_iteration else None
+            nxt = io.submit(load, 0) if num_iteration and not gpu_parse else None
             for it in range(num_iteration):
-                files, batched = nxt.result()
-                if it + 1 < num_iteration:
-                    nxt = io.submit(load, it + 1)
                 start_time = time.perf_counter()
-                out = quantize(model_params, random_key, batched)
+                out = None
+                if gpu_parse:
+                    files, out = gpu_batch(it)
+                if out is None:
+                    files, batched = nxt.result() if nxt is not None else load(it)
+                    nxt = None
+                    if not gpu_parse and it + 1 < num_iteration:
+                        nxt = io.submit(load, it + 1)
+                    start_time = time.perf_counter()
+                    out = quantize(model_params, random_key, batched)
                 tokens = out["tokens"].reshape(effective_batch_size, -1)
                 n_tok = out["n_tokens"].reshape(effective_batch_size)
                 names, arrays = [], []
