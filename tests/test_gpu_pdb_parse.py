@@ -138,7 +138,7 @@ def test_host_path_errors_are_the_host_parsers(tk, casp, tmp_path):
     bad = _write(tmp_path, "ins.pdb", ins)
     with pytest.raises(Exception, match="insertion code"):
         tk.tokenize_pdb_files([bad])
-    with pytest.raises(Exception, match="cannot open"):
+    with pytest.raises(FileNotFoundError):  # the binding sizes the token buffer from the files
         tk.tokenize_pdb_files([casp[0], str(tmp_path / "missing.pdb")])
     # the context keeps working after the errors
     _check_equal(tk, casp[:3], host_files=0)
