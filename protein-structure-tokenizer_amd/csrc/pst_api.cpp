@@ -1305,6 +1305,7 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
                     {(void**)&a.rec_run, sizeof(int32_t) * RB},
                     {(void**)&a.run_first, sizeof(int32_t) * RB},
                     {(void**)&a.run_out, sizeof(int32_t) * RB},
+                    {(void**)&a.run_type, (size_t)RB},
                     {(void**)&a.slot, sizeof(int32_t) * 37 * RB},
                     {(void**)&a.n_res, sizeof(int32_t) * 3 * n}};
     size_t total = 0;

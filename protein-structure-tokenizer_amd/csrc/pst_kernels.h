@@ -199,6 +199,7 @@ struct PdbScanArgs {
   int32_t* rec_run;          // residue run of the record
   int32_t* run_first;        // first record of each run
   int32_t* run_out;          // kept-residue ordinal of each run (-1: no atom37 atom)
+  int8_t* run_type;          // residue type of each run (0..19 the standard ones, 20 UNK)
   int32_t* slot;             // [runs][37] first record of each atom37 name
   int32_t* n_res;            // [n] kept residues
   int32_t* n_run;            // [n]

@@ -121,6 +121,7 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
   const int64_t lb = f0 + f, rb = a.rec_base[f];
   const int rec_cap = (int)(a.rec_base[f + 1] - rb);
   __shared__ int s_bad, s_start, s_stop, s_chain_seg[256];
+  __shared__ uint32_t s_line[PDB_THREADS][17];  // a record's first 64 bytes per thread (stride 17: no bank conflicts)
   if (tid == 0) {
     s_bad = 0;
     s_start = PDB_INT_MAX;
@@ -128,25 +129,42 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
   }
   for (int c = tid; c < 256; c += PDB_THREADS) s_chain_seg[c] = 0;
   __syncthreads();
-  // ---- lines: separators '\n' and '\r' counted per contiguous chunk, then their positions
-  const int chunk = (len + PDB_THREADS - 1) / PDB_THREADS;
-  const int c0 = min(len, tid * chunk), c1 = min(len, c0 + chunk);
-  int cnt = 0;
+  // ---- lines: the file's bytes as 16-byte words of the (256-aligned) text buffer, one word per
+  // thread per 16 KB tile (coalesced): separators '\n' / '\r' counted, scanned, and their line
+  // starts written in byte order
+  const int64_t w0 = f0 >> 4, w1 = (f0 + len + 15) >> 4;
+  const uint4* tw = reinterpret_cast<const uint4*>(a.text);
+  if (tid == 0) a.line_start[lb] = 0;
+  int at = 1;
   bool bad = false;
-  for (int i = c0; i < c1; ++i) {
-    const char c = tx[i];
-    if (c == '\n' || c == '\r') ++cnt;
-    else if (c < 0x20 || c > 0x7e) bad = true;
+  for (int64_t t0 = w0; t0 < w1; t0 += PDB_THREADS) {
+    const int64_t wi = t0 + tid;
+    const uint4 v = wi < w1 ? tw[wi] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+    uint32_t sep = 0;
+    int cnt = 0;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int64_t p = wi * 16 + b;
+      const uint32_t c = (d[b >> 2] >> (8 * (b & 3))) & 0xffu;
+      if (wi < w1 && p >= f0 && p < f0 + len) {
+        if (c == '\n' || c == '\r') {
+          sep |= 1u << b;
+          ++cnt;
+        } else if (c < 0x20u || c > 0x7eu) {
+          bad = true;
+        }
+      }
+    }
+    int tile = 0;
+    int q = at + block_scan(cnt, &tile);
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+      if ((sep >> b) & 1u) a.line_start[lb + q++] = (int)(wi * 16 + b - f0) + 1;
+    at += tile;
   }
   if (bad) s_bad = 1;
-  int n_sep = 0;
-  int at = block_scan(cnt, &n_sep) + 1;
-  if (tid == 0) a.line_start[lb] = 0;
-  for (int i = c0; i < c1; ++i) {
-    const char c = tx[i];
-    if (c == '\n' || c == '\r') a.line_start[lb + at++] = i + 1;
-  }
-  const int n_lines = n_sep + 1;  // the last line may be empty
+  const int n_lines = at;  // separators + 1 (the last line may be empty)
   __syncthreads();
   // ---- record kinds; the header ends at the first ATOM / HETATM / MODEL line
   for (int i = tid; i < n_lines; i += PDB_THREADS) {
@@ -185,7 +203,20 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
       continue;
     }
     const int s = a.line_start[lb + i], ll = line_end(a, lb, i, n_lines, len) - s;
-    const char* L = tx + s;
+    // the record's first 64 bytes into this thread's LDS row (17 independent dword loads, byte-
+    // aligned with alignbyte; reads past the line stay inside the scratch allocation and are never
+    // used: every column read below is < 54 <= ll or clipped to ll)
+    {
+      const int64_t pa = f0 + s;
+      const uint32_t* t32 = reinterpret_cast<const uint32_t*>(a.text) + (pa >> 2);
+      const uint32_t sh = (uint32_t)(pa & 3);
+      uint32_t dw[17];
+#pragma unroll
+      for (int j = 0; j < 17; ++j) dw[j] = t32[j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s_line[tid][j] = __builtin_amdgcn_alignbyte(dw[j + 1], dw[j], sh);
+    }
+    const char* L = reinterpret_cast<const char*>(s_line[tid]);
     bool ok = ll >= 54 && L[16] == ' ' && L[26] == ' ';
     double x = 0.0, y = 0.0, z = 0.0;
     int rs = 0;
@@ -262,6 +293,14 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
   for (int r = tid; r < n_run; r += PDB_THREADS) {
     const int k0 = a.run_first[rb + r], k1 = r + 1 < n_run ? a.run_first[rb + r + 1] : n_rec;
     for (int k = k0; k < k1; ++k) a.rec_run[rb + k] = r;
+    a.run_out[rb + r] = 0;  // set to 1 below by any record of an atom37 name
+    {  // residue type: the first record's name among the 20 standard ones, else UNK
+      const uint32_t rn = a.rec_name[rb + k0];
+      int rt = 20;
+      for (int q = 0; q < 20; ++q)
+        if (a.tab.res_key[q] == rn) rt = q;
+      a.run_type[rb + r] = (int8_t)rt;
+    }
     const uint8_t ch = a.rec_chain[rb + k0];
     if (r == 0 || a.rec_chain[rb + a.run_first[rb + r - 1]] != ch) {
       atomicAdd(&s_chain_seg[ch], 1);
@@ -278,16 +317,18 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
   // ---- atom slots: the first record of each atom37 name in its residue
   for (int k = tid; k < n_rec; k += PDB_THREADS) {
     const int at = a.rec_atom[rb + k];
-    if (at >= 0) atomicMin(&a.slot[37 * (rb + a.rec_run[rb + k]) + at], k);
+    if (at >= 0) {
+      const int r = a.rec_run[rb + k];
+      atomicMin(&a.slot[37 * (rb + r) + at], k);
+      a.run_out[rb + r] = 1;
+    }
   }
   __syncthreads();
   // ---- kept residues (at least one atom37 atom), numbered in file order
   int n_keep = 0;
   for (int t0 = 0; t0 < n_run; t0 += PDB_THREADS) {
     const int r = t0 + tid;
-    bool keep = false;
-    if (r < n_run)
-      for (int q = 0; q < 37 && !keep; ++q) keep = a.slot[37 * (rb + r) + q] != PDB_INT_MAX;
+    const bool keep = r < n_run && a.run_out[rb + r] != 0;
     int tile = 0;
     const int o = n_keep + block_scan(keep ? 1 : 0, &tile);
     if (r < n_run) a.run_out[rb + r] = keep ? o : -1;
@@ -306,15 +347,12 @@ __global__ __launch_bounds__(256) void k_pdb_write(PdbScanArgs a) {
   const int f = blockIdx.x;
   if (a.host_path[f]) return;
   const int64_t rb = a.rec_base[f], row0 = a.res_off[f];
-  const int n_run = a.n_run[f];
-  for (int e = threadIdx.x; e < n_run * 37; e += 256) {
+  const int n_el = a.n_run[f] * 37;
+  for (int e = blockIdx.y * 256 + threadIdx.x; e < n_el; e += gridDim.y * 256) {
     const int r = e / 37, at = e - 37 * r;
     const int o = a.run_out[rb + r];
     if (o < 0) continue;
-    const uint32_t rn = a.rec_name[rb + a.run_first[rb + r]];
-    int rt = 20;
-    for (int q = 0; q < 20; ++q)
-      if (a.tab.res_key[q] == rn) rt = q;
+    const int rt = a.run_type[rb + r];
     const int k = a.slot[37 * (rb + r) + at];
     const int64_t row = row0 + o;
     float* p = a.pos + (row * 37 + at) * 3;
@@ -331,12 +369,15 @@ __global__ __launch_bounds__(256) void k_pdb_write(PdbScanArgs a) {
   }
 }
 
+// k_pdb_write: workgroups per file (each a strided share of the file's residue-atom slots)
+constexpr int PDB_WRITE_SPLIT = 8;
+
 void launch_pdb_scan(const PdbScanArgs& a, int n_files, hipStream_t st) {
   hipLaunchKernelGGL(k_pdb_scan, dim3(n_files), dim3(PDB_THREADS), 0, st, a);
 }
 
 void launch_pdb_write(const PdbScanArgs& a, int n_files, hipStream_t st) {
-  hipLaunchKernelGGL(k_pdb_write, dim3(n_files), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_pdb_write, dim3(n_files, PDB_WRITE_SPLIT), dim3(256), 0, st, a);
 }
 
 }  // namespace pst
