@@ -266,7 +266,9 @@ int pst_tokenize_pdb_batch(pst_ctx* ctx, const pst_pdb_batch* b, uint32_t* token
  * are parsed by the native host parser instead, with its results and its errors (PST_E_INVALID +
  * the parser's message). Same rows as pst_pdb_parse_files + pst_tokenize_f32, bit for bit.
  * tokens_out [tokens_cap] receives R token slots (raw-offset layout, R = offsets_out[n]; a
- * residue needs >= 55 bytes of file, so sum(file sizes) / 54 + n always suffices),
+ * residue needs >= 55 bytes of file, so sum(file sizes) / 54 + n always suffices; when tokens_cap
+ * is smaller than R the call fails with PST_E_INVALID "token buffer too small" and, if offsets_out
+ * is given, offsets_out[n] = R so the caller can retry with a buffer of that size),
  * n_tokens_out / n_nodes_out [n] and offsets_out [n+1] may be NULL. */
 int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, int32_t n_threads,
                            uint32_t* tokens_out, int64_t tokens_cap, int32_t* n_tokens_out, int32_t* n_nodes_out,

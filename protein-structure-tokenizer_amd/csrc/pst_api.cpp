@@ -11,7 +11,9 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <atomic>
 
@@ -259,6 +261,7 @@ struct pst_ctx {
   int64_t down_coop = -2;    // PST_DOWN_COOP: k_down_coop iff n_tiles <= this; -1 = default; -2 = not read yet
   int64_t down_pair = -2;    // PST_DOWN_PAIR: 1 = k_down_pair whenever not coop (df 1), 0 = never; -1 = one round of tiles
   int32_t* h_counts = nullptr;  // pinned host copy of [n_tok | n_nodes] (cap_B each)
+  uint32_t* h_tokens = nullptr;  // pinned landing buffer of the token D2H (cap_R)
   int32_t last_down_form = 0;  // pst::DOWN_* of the last run (pst_debug_fetch 20, plan[19])
   int64_t half_tasks = -2;   // PST_HALF_TASKS: 1 = fused layers always two waves per task, 0 = never; -1 = policy
   int64_t mpnn_qwaves = -2;  // PST_MPNN_QWAVES: 4 = two 4-wave queue workgroups per CU; else one 8-wave workgroup
@@ -552,6 +555,9 @@ int ensure_workspace(pst_ctx* ctx, int64_t R, int B) {
   if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
   ctx->h_counts = nullptr;
   if (hipHostMalloc((void**)&ctx->h_counts, sizeof(int32_t) * 2 * B) != hipSuccess) ctx->h_counts = nullptr;
+  if (ctx->h_tokens) (void)hipHostFree(ctx->h_tokens);
+  ctx->h_tokens = nullptr;
+  if (hipHostMalloc((void**)&ctx->h_tokens, sizeof(uint32_t) * Rpad) != hipSuccess) ctx->h_tokens = nullptr;
   ctx->ws_bytes = total;
   const char* dbg = getenv("PST_DEBUG");
   if (dbg && dbg[0] == '1') {
@@ -961,6 +967,7 @@ int pst_destroy(pst_ctx* ctx) {
   for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_U, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
   if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
+  if (ctx->h_tokens) (void)hipHostFree(ctx->h_tokens);
   if (ctx->h_stage_pos) (void)hipHostFree(ctx->h_stage_pos);
   if (ctx->h_stage_flags) (void)hipHostFree(ctx->h_stage_flags);
   if (ctx->h_text) (void)hipHostFree(ctx->h_text);
@@ -1062,6 +1069,41 @@ std::vector<int32_t> plan_chunks(pst_ctx* ctx, const int64_t* offsets, int32_t n
 
 // pst_tokenize / pst_tokenize_f32: `atom_pos` holds [R,37,3] doubles, or floats when `f32`
 // (copied as they are — half the H2D bytes — and widened to f64 on load in k_prep).
+// Token ids and per-protein counts of the last run() to the caller's (pageable) host buffers:
+// one DMA each into the context's page-locked buffers, one stream sync, then host copies (the
+// token rows on the host pool above 256 KB) — a D2H into pageable memory is staged and blocks the
+// host per copy.
+int results_to_host(pst_ctx* ctx, int64_t R, int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out,
+                    int32_t* n_nodes_out) {
+  auto& w = ctx->w;
+  hipStream_t st = ctx->stream;
+  uint32_t* tok_land = ctx->h_tokens && R <= ctx->cap_R ? ctx->h_tokens : tokens_out;
+  HIPCHK(hipMemcpyAsync(tok_land, w.tokens, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, st));
+  // both count arrays in one copy into pinned memory (one DMA instead of two staged ones)
+  const bool counts = n_tokens_out || n_nodes_out;
+  const int64_t capB = ctx->cap_B;
+  if (counts && ctx->h_counts) {
+    HIPCHK(hipMemcpyAsync(ctx->h_counts, w.n_tok, sizeof(int32_t) * (capB + n_prot), hipMemcpyDeviceToHost, st));
+  } else if (counts) {
+    if (n_tokens_out) HIPCHK(hipMemcpyAsync(n_tokens_out, w.n_tok, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, st));
+    if (n_nodes_out) HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (tok_land != tokens_out) {
+    constexpr int64_t PART = 1 << 16;  // tokens per host copy task (256 KB)
+    const int parts = (int)((R + PART - 1) / PART);
+    pst::HostPool::get().run(parts, std::min(parts, 8), [&](int i) {
+      const int64_t a = (int64_t)i * PART, b = std::min<int64_t>(R, a + PART);
+      std::memcpy(tokens_out + a, tok_land + a, sizeof(uint32_t) * (b - a));
+    });
+  }
+  if (counts && ctx->h_counts) {
+    if (n_tokens_out) std::memcpy(n_tokens_out, ctx->h_counts, sizeof(int32_t) * n_prot);
+    if (n_nodes_out) std::memcpy(n_nodes_out, ctx->h_counts + capB, sizeof(int32_t) * n_prot);
+  }
+  return PST_OK;
+}
+
 int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* atom_flags, const int64_t* offsets,
                   int32_t n_prot, uint32_t* tokens_out, int32_t* n_tokens_out, int32_t* n_nodes_out) {
   if (!ctx) return PST_E_INVALID;
@@ -1175,25 +1217,7 @@ int tokenize_host(pst_ctx* ctx, const void* atom_pos, bool f32, const uint8_t* a
     ctx->chunked_last = true;
   }
   hipLaunchKernelGGL(k_ntok, dim3((n_prot + 255) / 256), dim3(256), 0, ctx->stream, w.n_nodes, w.n_tok, n_prot, ctx->df);
-  HIPCHK(hipMemcpyAsync(tokens_out, w.tokens, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, ctx->stream));
-  // both count arrays in one copy into pinned memory (one DMA instead of two staged ones)
-  const bool counts = n_tokens_out || n_nodes_out;
-  const int64_t capB = ctx->cap_B;
-  if (counts && ctx->h_counts)
-    HIPCHK(hipMemcpyAsync(ctx->h_counts, w.n_tok, sizeof(int32_t) * (capB + n_prot), hipMemcpyDeviceToHost,
-                          ctx->stream));
-  else if (counts) {
-    if (n_tokens_out)
-      HIPCHK(hipMemcpyAsync(n_tokens_out, w.n_tok, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
-    if (n_nodes_out)
-      HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n_prot, hipMemcpyDeviceToHost, ctx->stream));
-  }
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  if (counts && ctx->h_counts) {
-    if (n_tokens_out) std::memcpy(n_tokens_out, ctx->h_counts, sizeof(int32_t) * n_prot);
-    if (n_nodes_out) std::memcpy(n_nodes_out, ctx->h_counts + capB, sizeof(int32_t) * n_prot);
-  }
-  return PST_OK;
+  return results_to_host(ctx, R, n_prot, tokens_out, n_tokens_out, n_nodes_out);
 }
 
 }  // namespace
@@ -1248,13 +1272,27 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
   HIPCHK(hipSetDevice(ctx->device));
   const int threads = std::max(1, n_threads);
   auto& pool = pst::HostPool::get();
-  // ---- file sizes, then the texts read straight into page-locked memory
+  // ---- files opened and sized, then their texts read straight into page-locked memory
   std::vector<int64_t> fsz(n, 0);
+  std::vector<int> fds(n, -1);
+  struct FdClose {
+    std::vector<int>& f;
+    ~FdClose() {
+      for (int& d : f)
+        if (d >= 0) ::close(d), d = -1;
+    }
+  } fd_close{fds};
   std::atomic<int> bad_file(-1);
   pool.run(n, threads, [&](int i) {
+    const int fd = ::open(paths[i], O_RDONLY | O_CLOEXEC);
     struct stat st;
-    if (stat(paths[i], &st) != 0) bad_file.store(i);
-    else fsz[i] = (int64_t)st.st_size;
+    if (fd < 0 || fstat(fd, &st) != 0) {
+      if (fd >= 0) ::close(fd);
+      bad_file.store(i);
+      return;
+    }
+    fds[i] = fd;
+    fsz[i] = (int64_t)st.st_size;
   });
   if (bad_file.load() >= 0) return fail(ctx, PST_E_INVALID, std::string("cannot open ") + paths[bad_file.load()]);
   std::vector<int64_t> foff(n + 1, 0), rbase(n + 1, 0);
@@ -1272,14 +1310,15 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
     ctx->h_text_cap = cap;
   }
   pool.run(n, threads, [&](int i) {
-    FILE* fh = fopen(paths[i], "rb");
-    if (!fh) {
-      bad_file.store(i);
-      return;
+    int64_t got = 0;
+    while (got < fsz[i]) {
+      const ssize_t r = ::pread(fds[i], ctx->h_text + foff[i] + got, (size_t)(fsz[i] - got), (off_t)got);
+      if (r <= 0) break;
+      got += r;
     }
-    const size_t got = fsz[i] ? fread(ctx->h_text + foff[i], 1, (size_t)fsz[i], fh) : 0;
-    fclose(fh);
-    if ((int64_t)got != fsz[i]) bad_file.store(i);
+    ::close(fds[i]);
+    fds[i] = -1;
+    if (got != fsz[i]) bad_file.store(i);
   });
   if (bad_file.load() >= 0) return fail(ctx, PST_E_INVALID, std::string("cannot read ") + paths[bad_file.load()]);
   // ---- device scratch of the GPU parse (one grow-only allocation)
@@ -1395,7 +1434,10 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
   int rc = validate(ctx, off.data(), n);
   if (rc) return rc;
   const int64_t R = off[n];
-  if (R > tokens_cap) return fail(ctx, PST_E_INVALID, "token buffer too small");
+  if (R > tokens_cap) {
+    if (offsets_out) offsets_out[n] = R;
+    return fail(ctx, PST_E_INVALID, "token buffer too small");
+  }
   rc = ensure_workspace(ctx, R, n);
   if (rc) return rc;
   auto& w = ctx->w;
@@ -1430,16 +1472,8 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
   rc = run(ctx, nullptr, w.flags, off.data(), n, w.tokens, w.n_tok, w.n_nodes, false, 0, a.pos);
   if (rc) return rc;
   hipLaunchKernelGGL(k_ntok, dim3((n + 255) / 256), dim3(256), 0, st, w.n_nodes, w.n_tok, n, ctx->df);
-  HIPCHK(hipMemcpyAsync(tokens_out, w.tokens, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, st));
-  if ((n_tokens_out || n_nodes_out) && ctx->h_counts) {
-    HIPCHK(hipMemcpyAsync(ctx->h_counts, w.n_tok, sizeof(int32_t) * (ctx->cap_B + n), hipMemcpyDeviceToHost, st));
-  } else {
-    if (n_tokens_out) HIPCHK(hipMemcpyAsync(n_tokens_out, w.n_tok, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
-    if (n_nodes_out) HIPCHK(hipMemcpyAsync(n_nodes_out, w.n_nodes, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
-  }
-  HIPCHK(hipStreamSynchronize(st));
-  if (n_tokens_out && ctx->h_counts) std::memcpy(n_tokens_out, ctx->h_counts, sizeof(int32_t) * n);
-  if (n_nodes_out && ctx->h_counts) std::memcpy(n_nodes_out, ctx->h_counts + ctx->cap_B, sizeof(int32_t) * n);
+  rc = results_to_host(ctx, R, n, tokens_out, n_tokens_out, n_nodes_out);
+  if (rc) return rc;
   if (offsets_out) std::memcpy(offsets_out, off.data(), sizeof(int64_t) * (n + 1));
   return PST_OK;
 }

@@ -60,6 +60,18 @@ __device__ int block_scan(int v, int* total) {
   return base + x - v;
 }
 
+constexpr int TILE_BYTES = 64 * PDB_THREADS;  // the lines pass's tile
+
+// 0x80 in each byte of x equal to the byte of c (c: one byte value replicated), exact
+__device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint32_t c) {
+  const uint32_t y = x ^ c;
+  return ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;
+}
+// the four 0x80 flags of a SWAR mask as bits 0..3 (byte order)
+__device__ __forceinline__ uint32_t swar_bits(uint32_t m) {
+  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
+
 __device__ __forceinline__ bool is6(const char* p, const char* s) {
   return p[0] == s[0] && p[1] == s[1] && p[2] == s[2] && p[3] == s[3] && p[4] == s[4] && p[5] == s[5];
 }
@@ -121,7 +133,11 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
   const int64_t lb = f0 + f, rb = a.rec_base[f];
   const int rec_cap = (int)(a.rec_base[f + 1] - rb);
   __shared__ int s_bad, s_start, s_stop, s_chain_seg[256];
-  __shared__ uint32_t s_line[PDB_THREADS][17];  // a record's first 64 bytes per thread (stride 17: no bank conflicts)
+  // LDS: the text tile of the lines pass (64 KB), then each record's first 64 bytes per thread
+  // (stride 17 dwords: no bank conflicts)
+  __shared__ uint32_t s_buf[PDB_THREADS * 17];
+  uint32_t(*s_line)[17] = reinterpret_cast<uint32_t(*)[17]>(s_buf);
+  const char* s_tile = reinterpret_cast<const char*>(s_buf);
   if (tid == 0) {
     s_bad = 0;
     s_start = PDB_INT_MAX;
@@ -129,58 +145,94 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
   }
   for (int c = tid; c < 256; c += PDB_THREADS) s_chain_seg[c] = 0;
   __syncthreads();
-  // ---- lines: the file's bytes as 16-byte words of the (256-aligned) text buffer, one word per
-  // thread per 16 KB tile (coalesced): separators '\n' / '\r' counted, scanned, and their line
-  // starts written in byte order
+  // ---- lines and their record kinds: the file's bytes as 16-byte words of the (256-aligned)
+  // text buffer, 64 contiguous bytes per thread per 64 KB tile (the next tile's words loaded
+  // during this one's scan): separators '\n' / '\r' counted, scanned, and at each one the line
+  // start it opens and that line's kind written. The header ends at the first ATOM / HETATM /
+  // MODEL line. A kind needs its 6 bytes inside the file (a match never holds a separator, so it
+  // lies inside the line).
+  // tile_lo: the file position of the LDS tile's byte 0 (the tile holds TILE_BYTES bytes)
+  auto kind_at = [&](int st, int64_t tile_lo) -> uint8_t {
+    if (st + 6 > len) return K_OTHER;
+    const int64_t o = f0 + st - tile_lo;
+    const char* p = o >= 0 && o + 6 <= TILE_BYTES ? s_tile + o : tx + st;
+    if (is6(p, "ATOM  ")) return K_ATOM;
+    if (is6(p, "HETATM")) return K_HETATM;
+    if (is6(p, "MODEL ")) return K_MODEL;
+    if (is6(p, "ENDMDL")) return K_ENDMDL;
+    if (is6(p, "END   ") || is6(p, "CONECT")) return K_STOP;
+    return K_OTHER;
+  };
+  auto note_kind = [&](int i, int st, int64_t tile_lo) {
+    const uint8_t k = kind_at(st, tile_lo);
+    a.line_kind[lb + i] = k;
+    // s_start only falls: past the header no atomic is issued
+    if ((k == K_ATOM || k == K_HETATM || k == K_MODEL) && i < *(volatile int*)&s_start) atomicMin(&s_start, i);
+  };
   const int64_t w0 = f0 >> 4, w1 = (f0 + len + 15) >> 4;
   const uint4* tw = reinterpret_cast<const uint4*>(a.text);
-  if (tid == 0) a.line_start[lb] = 0;
+  constexpr int TW = 4 * PDB_THREADS;  // words per tile
+  if (tid == 0) {
+    a.line_start[lb] = 0;
+    note_kind(0, 0, -TILE_BYTES);  // (not in the tile: read from HBM)
+  }
   int at = 1;
   bool bad = false;
-  for (int64_t t0 = w0; t0 < w1; t0 += PDB_THREADS) {
-    const int64_t wi = t0 + tid;
-    const uint4 v = wi < w1 ? tw[wi] : make_uint4(0u, 0u, 0u, 0u);
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-    uint32_t sep = 0;
-    int cnt = 0;
+  uint4 cur[4], nxt[4];
 #pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      const int64_t p = wi * 16 + b;
-      const uint32_t c = (d[b >> 2] >> (8 * (b & 3))) & 0xffu;
-      if (wi < w1 && p >= f0 && p < f0 + len) {
-        if (c == '\n' || c == '\r') {
-          sep |= 1u << b;
-          ++cnt;
-        } else if (c < 0x20u || c > 0x7eu) {
-          bad = true;
-        }
-      }
+  for (int q = 0; q < 4; ++q) {
+    const int64_t wi = w0 + 4 * tid + q;
+    cur[q] = wi < w1 ? tw[wi] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  for (int64_t t0 = w0; t0 < w1; t0 += TW) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t wi = t0 + TW + 4 * tid + q;
+      nxt[q] = wi < w1 ? tw[wi] : make_uint4(0u, 0u, 0u, 0u);
     }
+    const int64_t pb = (t0 + 4 * tid) * 16;  // absolute position of this thread's byte 0
+    // this thread's 64 bytes into the LDS tile (read by the kinds below after the scan's barrier)
+    uint4* tl = reinterpret_cast<uint4*>(s_buf) + 4 * tid;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tl[q] = cur[q];
+    // bytes of the file within this thread's 64: [lo, hi)
+    const int lo = (int)max<int64_t>(0, min<int64_t>(64, f0 - pb));
+    const int hi = (int)max<int64_t>(0, min<int64_t>(64, f0 + len - pb));
+    const uint64_t in = hi <= lo ? 0ull : ((hi >= 64 ? ~0ull : (1ull << hi) - 1ull) & ~((1ull << lo) - 1ull));
+    // per-byte flags four bytes at a time (exact SWAR tests): separators, and bytes outside
+    // printable ASCII other than them
+    uint64_t sep = 0, bad_m = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint4& v = cur[j >> 2];
+      const uint32_t x = (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
+      const uint32_t s_m = swar_eq(x, 0x0a0a0a0au) | swar_eq(x, 0x0d0d0d0du);
+      const uint32_t lo7 = x & 0x7f7f7f7fu;
+      const uint32_t lt20 = ~(lo7 + 0x60606060u) & ~x & 0x80808080u;  // byte < 0x20
+      const uint32_t ge7f = (x & 0x80808080u) | swar_eq(x, 0x7f7f7f7fu);  // byte > 0x7e
+      sep |= (uint64_t)swar_bits(s_m) << (4 * j);
+      bad_m |= (uint64_t)swar_bits((lt20 | ge7f) & ~s_m) << (4 * j);
+    }
+    sep &= in;
+    if (bad_m & in) bad = true;
+    const int cnt = __builtin_popcountll(sep);
     int tile = 0;
     int q = at + block_scan(cnt, &tile);
-#pragma unroll
-    for (int b = 0; b < 16; ++b)
-      if ((sep >> b) & 1u) a.line_start[lb + q++] = (int)(wi * 16 + b - f0) + 1;
+    while (sep) {
+      const int b = __builtin_ctzll(sep);
+      sep &= sep - 1;
+      const int st = (int)(pb + b - f0) + 1;
+      a.line_start[lb + q] = st;
+      note_kind(q, st, t0 * 16);
+      ++q;
+    }
     at += tile;
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) cur[q2] = nxt[q2];
+    __syncthreads();  // the LDS tile is rewritten next
   }
   if (bad) s_bad = 1;
   const int n_lines = at;  // separators + 1 (the last line may be empty)
-  __syncthreads();
-  // ---- record kinds; the header ends at the first ATOM / HETATM / MODEL line
-  for (int i = tid; i < n_lines; i += PDB_THREADS) {
-    const int s = a.line_start[lb + i], ll = line_end(a, lb, i, n_lines, len) - s;
-    uint8_t k = K_OTHER;
-    if (ll >= 6) {
-      const char* p = tx + s;
-      if (is6(p, "ATOM  ")) k = K_ATOM;
-      else if (is6(p, "HETATM")) k = K_HETATM;
-      else if (is6(p, "MODEL ")) k = K_MODEL;
-      else if (is6(p, "ENDMDL")) k = K_ENDMDL;
-      else if (is6(p, "END   ") || is6(p, "CONECT")) k = K_STOP;
-    }
-    a.line_kind[lb + i] = k;
-    if (k == K_ATOM || k == K_HETATM || k == K_MODEL) atomicMin(&s_start, i);
-  }
   __syncthreads();
   const int start = s_start;
   for (int i = tid; i < n_lines; i += PDB_THREADS)
@@ -189,9 +241,23 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
   const int stop = min(s_stop, n_lines);
   // ---- ATOM / HETATM records of [start, stop) in line order, fields parsed
   int n_rec = 0;
+  // each line's kind / start / end loaded one iteration ahead
+  auto line_info = [&](int i, uint8_t& k, int& st, int& en) {
+    k = K_OTHER;
+    st = en = 0;
+    if (i < stop) {
+      k = a.line_kind[lb + i];
+      st = a.line_start[lb + i];
+      en = line_end(a, lb, i, n_lines, len);
+    }
+  };
+  uint8_t k_nx;
+  int s_nx, e_nx;
+  line_info(start + tid, k_nx, s_nx, e_nx);
   for (int t0 = start; t0 < stop; t0 += PDB_THREADS) {
-    const int i = t0 + tid;
-    const uint8_t k = i < stop ? a.line_kind[lb + i] : K_OTHER;
+    const uint8_t k = k_nx;
+    const int s = s_nx, ll = e_nx - s_nx;
+    line_info(t0 + PDB_THREADS + tid, k_nx, s_nx, e_nx);
     if (k == K_MODEL || k == K_ENDMDL) s_bad = 1;
     const bool rec = k == K_ATOM || k == K_HETATM;
     int tile = 0;
@@ -202,7 +268,6 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
       s_bad = 1;
       continue;
     }
-    const int s = a.line_start[lb + i], ll = line_end(a, lb, i, n_lines, len) - s;
     // the record's first 64 bytes into this thread's LDS row (17 independent dword loads, byte-
     // aligned with alignbyte; reads past the line stay inside the scratch allocation and are never
     // used: every column read below is < 54 <= ll or clipped to ll)

@@ -297,6 +297,7 @@ class Tokenizer:
             raise_for(rc, L.pst_create_error().decode())
         self._h = h
         self.device = device
+        self._pdb_tok = np.empty(1 << 16, np.uint32)  # tokenize_pdb_files' token buffer (grown on demand)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -349,17 +350,29 @@ class Tokenizer:
         """PDB files → (tokens [R] uint32 raw-offset layout, n_tokens [n], n_nodes [n], offsets
         [n+1]) through pst_tokenize_pdb_files: the texts parsed on the GPU straight into the
         tokenizer's inputs (files outside the GPU fast path through the native host parser)."""
-        enc = [os.fsencode(p) for p in paths]
-        n = len(enc)
-        arr = (ctypes.c_char_p * max(n, 1))(*enc)
-        cap = sum(os.path.getsize(p) for p in paths) // 54 + n + 1
-        tok = np.empty(cap, np.uint32)
+        # the paths as one NUL-separated blob and a pointer array into it (a ctypes c_char_p array
+        # costs ~1 us per path); the token buffer is the context's, grown when the call reports a
+        # larger R (offsets[n]), so no file is stat'ed here
+        n = len(paths)
+        enc = [os.fsencode(p) + b"\0" for p in paths]
+        blob = np.frombuffer(b"".join(enc), np.uint8)
+        starts = np.zeros(max(n, 1), np.uint64)
+        if n:
+            starts[1:n] = np.cumsum([len(e) for e in enc[:-1]], dtype=np.uint64)
+        ptrs = starts + np.uint64(blob.ctypes.data)
         nt = np.empty(n, np.int32)
         nn = np.empty(n, np.int32)
         off = np.zeros(n + 1, np.int64)
-        self._check(lib().pst_tokenize_pdb_files(self._h, arr, n, n_threads, _ptr(tok), cap, _ptr(nt), _ptr(nn),
-                                                 _ptr(off)))
-        return tok[:int(off[-1])], nt, nn, off
+        for _ in range(2):
+            tok = self._pdb_tok
+            rc = lib().pst_tokenize_pdb_files(self._h, _ptr(ptrs), n, n_threads, _ptr(tok), tok.size, _ptr(nt), _ptr(nn),
+                                              _ptr(off))
+            if rc == PST_E_INVALID and n and int(off[-1]) > tok.size:
+                self._pdb_tok = np.empty(int(off[-1]) * 2, np.uint32)
+                continue
+            self._check(rc)
+            break
+        return tok[:int(off[-1])].copy(), nt, nn, off
 
     def pdb_files_host_parsed(self) -> int:
         """Files of the last tokenize_pdb_files call that took the host parser."""

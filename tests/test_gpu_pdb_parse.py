@@ -54,8 +54,12 @@ def _check_equal(tk, paths, host_files):
 
 def test_casp14_files_parsed_on_gpu_equal_host_parser(tk, casp):
     """All 31 CASP14 structures take the GPU path (T1024's header has '\\r' line breaks) and give
-    the host parser's rows bit for bit, and the same tokens."""
+    the host parser's rows bit for bit, and the same tokens. Then once more from a token buffer too
+    small for the batch: the call reports R, the binding grows its buffer and repeats it."""
     _check_equal(tk, casp, host_files=0)
+    tk._pdb_tok = np.empty(16, np.uint32)
+    _check_equal(tk, casp, host_files=0)
+    assert tk._pdb_tok.size >= 5618
 
 
 def _lines(path):
@@ -138,7 +142,7 @@ def test_host_path_errors_are_the_host_parsers(tk, casp, tmp_path):
     bad = _write(tmp_path, "ins.pdb", ins)
     with pytest.raises(Exception, match="insertion code"):
         tk.tokenize_pdb_files([bad])
-    with pytest.raises(FileNotFoundError):  # the binding sizes the token buffer from the files
+    with pytest.raises(ValueError, match="cannot open"):
         tk.tokenize_pdb_files([casp[0], str(tmp_path / "missing.pdb")])
     # the context keeps working after the errors
     _check_equal(tk, casp[:3], host_files=0)
