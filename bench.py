@@ -412,13 +412,19 @@ def cpu_baselines(args, samples, blob, levels, pos, flags, off, gpu_tok, plan=No
         # and not another; every difference is listed with its reference margin
         ref = _reference_sample(args)
         if ref is not None:
+            import refwide
             ids_s = [ref_ids[i] for i in csel] if ref_ids is not None else list(csel)
             keep = [k for k, p in enumerate(ids_s) if p in ref.index]
-            rr = ref.compare([ids_s[k] for k in keep], [toks[k][:ref.n_tokens(ids_s[k])] for k in keep])
+            rr = ref.compare([ids_s[k] for k in keep], [toks[k][:ref.n_tokens(ids_s[k])] for k in keep],
+                             known=refwide.KNOWN_CPU_BASELINE_CASES)
             out[threads]["tokens_identical_to_reference"] = f"{rr['identical']} / {rr['tokens']}"
             out[threads]["mismatches_vs_reference"] = [
                 {k: m[k] for k in ("protein", "token", "ref_margin", "dim") if k in m} for m in rr["mismatches"]]
             out[threads]["unexplained_vs_reference"] = len(rr["unexplained"])
+            # every flip must be a listed known case (refwide.KNOWN_CPU_BASELINE_CASES), and every
+            # listed case of the sample must still flip
+            out[threads]["unlisted_vs_reference"] = len(rr["unlisted"])
+            out[threads]["known_cases_not_flipped"] = rr["missing_known"]
     cfg2 = {}
     if casp is not None and args.codebook == 4096 and args.df == 1:
         cpos, cflags, coff, ctok = casp

@@ -22,8 +22,13 @@ CLOSE = 1e-4
 # The headline workload's tokens that a float32 implementation resolves to the other side of a
 # rounding boundary than the reference's float64 evaluation: (sample, protein, token) -> the latent
 # dim whose margin our deviation exceeds. Every other token must be identical; an unlisted flip, or
-# a listed one that no longer flips, fails the tests.
+# a listed one that no longer flips, fails the tests. Measured on all 1 024
+# proteins (262 144 tokens): this one case.
 KNOWN_BOUNDARY_CASES = {("bench256", 924, 3): 5}
+# The same list for the CPU baseline bench.py times (oracle/reference_as_computed.py, the reference's
+# computation in PyTorch-CPU float32, on every 16th protein): its float32 sums flip the workload's
+# closest token (margin 8.8e-8), which the GPU path resolves as the reference does.
+KNOWN_CPU_BASELINE_CASES = {("bench256", 352, 221): 2}
 # log10 bins of the margin histogram: [0, 1e-7), [1e-7, 1e-6), ..., [1e-1, 0.5]
 EDGES = [0.0, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2, 1e-1, 0.5000001]
 
@@ -156,14 +161,15 @@ class BenchSample:
         i = self.index[int(p)]
         return int(self.tok_off[i + 1] - self.tok_off[i])
 
-    def compare(self, prots, ours, bounded=None):
+    def compare(self, prots, ours, bounded=None, known=None):
         """Exact match of `ours` (token ids per protein of `prots`) against the reference; with
         `bounded` (our FSQ-bounded latents per protein) the deviation |b_ours - b_ref| on every
         close token. Each mismatch is listed with its reference margin, the dim whose rounding
         differs and our deviation there; `unexplained` lists mismatches whose margin is not below
         CLOSE or not below our deviation (a real error, never rounding), `unlisted` the ones missing
         from KNOWN_BOUNDARY_CASES, `missing_known` the listed cases of these proteins that did not
-        flip."""
+        flip. `known` replaces KNOWN_BOUNDARY_CASES (KNOWN_CPU_BASELINE_CASES for the CPU baseline)."""
+        known = KNOWN_BOUNDARY_CASES if known is None else known
         close_pos = {int(f): j for j, f in enumerate(self.close)}
         n_tok = n_eq = n_close = 0
         mism, unexplained, unlisted = [], [], []
@@ -207,11 +213,11 @@ class BenchSample:
                         rec["our_deviation"] = float(abs(bo[t, d] - bref[d]))
                 ok = f in close_pos and ("our_deviation" not in rec or rec["our_deviation"] > rec["ref_margin"])
                 (mism if ok else unexplained).append(rec)
-                if KNOWN_BOUNDARY_CASES.get((self.name, int(p), int(t))) != rec.get("dim"):
+                if known.get((self.name, int(p), int(t))) != rec.get("dim"):
                     unlisted.append(rec)
         held = {int(p) for p in prots}
         flipped = {(r["protein"], r["token"]) for r in mism + unexplained}
-        missing = [list(k) for k in KNOWN_BOUNDARY_CASES
+        missing = [list(k) for k in known
                    if k[0] == self.name and k[1] in held and (k[1], k[2]) not in flipped]
         mall = np.concatenate(mm_all) if mm_all else np.zeros(0)
         mbad = np.concatenate(mm_bad) if mm_bad else np.zeros(0)
