@@ -106,6 +106,44 @@ def test_default_pipeline_policy_matches_one_shot():
     assert np.array_equal(tok, tok1) and np.array_equal(nt, nt1) and np.array_equal(nn, nn1)
 
 
+def test_pipeline_policy_knobs_keep_the_bits(monkeypatch):
+    """The remaining schedule knobs the A/B tools set, forced away from their policy values on the
+    same inputs, change only the schedule: a first chunk of two rounds growing 2x per chunk with no
+    minimum (PST_H2D_FIRST_ROUNDS / PST_H2D_GROWTH / PST_H2D_MIN_ROUNDS: 6 rounds as 2 + 4), and the
+    split schedule's edge waves at several blocks per wave (PST_EDGE_WAVES), against unpipelined
+    calls: same token ids and counts."""
+    from pst_amd._native import Tokenizer
+    samples = synthetic.synthetic_batch(768, 256, seed=4343)
+    pos, flags, off = pack_samples(samples)
+    t1 = _ctx(1)
+    tok1, nt1, nn1 = t1.tokenize_packed(pos, flags, off)
+    t1.close()
+    os.environ.pop("PST_H2D_CHUNKS")
+    for k, v in (("PST_H2D_FIRST_ROUNDS", "2"), ("PST_H2D_GROWTH", "2"), ("PST_H2D_MIN_ROUNDS", "1")):
+        monkeypatch.setenv(k, v)
+    t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
+    tok, nt, nn = t.tokenize_packed(pos, flags, off)
+    plan = t.last_plan_detail()
+    t.close()
+    assert plan["chunks"] == 2 and plan["cuts"] == [0, 256, 768], plan
+    assert np.array_equal(tok, tok1) and np.array_equal(nt, nt1) and np.array_equal(nn, nn1)
+    # split schedule (small batch) with ~4 blocks per edge wave against its default of one
+    small = synthetic.synthetic_batch(24, 256, seed=4444)
+    spos, sflags, soff = pack_samples(small)
+    outs = []
+    for ew in (None, "2000"):
+        if ew is None:
+            monkeypatch.delenv("PST_EDGE_WAVES", raising=False)
+        else:
+            monkeypatch.setenv("PST_EDGE_WAVES", ew)
+        t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
+        outs.append(t.tokenize_packed(spos, sflags, soff))
+        assert t.last_plan_detail()["schedules"] == ["split"]
+        t.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("chunks", [1, 3])
 def test_f32_positions_match_f64(chunks):
     """pst_tokenize_f32 (float32 positions, widened to f64 in k_prep) vs pst_tokenize on the same
