@@ -49,8 +49,31 @@ body = body.replace("    node_update_pair<LAYER>(a, g0, hh, lds_scratch[w & 2]);
                     "    WST(28);\n    node_update_pair<LAYER>(a, g0, hh, lds_scratch[w & 2]);\n    WST(29);\n    cs.stop(a.clk);", 1)
 assert body.count("WST(") == 6, body.count("WST(")
 s = s[:i] + body + s[j:]
+# node_update_pair phases: stamps 8 + k of a per-wave side array g_nst (after the x exchange, LN0,
+# each FFN chunk, the residual exchange, LN1 + h store, the projections)
+rep("__device__ unsigned long long g_wst[3][2048][32];\n",
+    "__device__ unsigned long long g_wst[3][2048][32];\n__device__ unsigned long long g_nst[3][2048][16];\n")
+i = s.index("template <int LAYER>\n__device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, int h, float* xs) {")
+j = s.index("template <int LAYER>\n__global__ __launch_bounds__(256, 1) void k_mpnn_node_coop")
+nb = s[i:j]
+nb = nb.replace("  const int lane = lane_id();\n", "  const int lane = lane_id();\n  const int64_t nw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);\n"
+                "#define NST(k) if (lane == 0 && nw < 2048) g_nst[LAYER][nw][k] = __builtin_amdgcn_s_memrealtime();\n  NST(0);\n", 1)
+nb = nb.replace("    pair_exchange(x, xp0, xp1, xs, h);\n  }\n  tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0\n",
+                "    pair_exchange(x, xp0, xp1, xs, h);\n  }\n  NST(1);\n  tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0\n  NST(2);\n", 1)
+nb = nb.replace("      blk_gemm(out1, hid, a.ff_w2 + ck * 64 * 64, b1);\n    }\n  }\n",
+                "      blk_gemm(out1, hid, a.ff_w2 + ck * 64 * 64, b1);\n    }\n    NST(3 + ck);\n  }\n", 1)
+nb = nb.replace("  tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1\n", "  NST(7);\n  tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1\n", 1)
+nb = nb.replace("  if (a.P_out) {\n#pragma unroll 1\n    for (int p = 0; p < 4; ++p) {\n      f32x16 pr0, pr1;",
+                "  NST(8);\n  if (a.P_out) {\n#pragma unroll 1\n    for (int p = 0; p < 4; ++p) {\n      f32x16 pr0, pr1;", 1)
+nb = nb.rstrip()
+assert nb.endswith("}"), nb[-40:]
+nb = nb[:-1] + "  NST(9);\n#undef NST\n}\n\n"
+assert nb.count("NST(") == 8, nb.count("NST(")
+s = s[:i] + nb + s[j:]
 s = s.replace("void launch_mpnn(", 'extern "C" int pst_x_wave_stamps(unsigned long long* out) {\n'
               "  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wst), sizeof(g_wst)) == hipSuccess ? 0 : -1;\n}\n"
+              'extern "C" int pst_x_node_stamps(unsigned long long* out) {\n'
+              "  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nst), sizeof(g_nst)) == hipSuccess ? 0 : -1;\n}\n"
               "void launch_mpnn(", 1)
 open(p, "w").write(s)
 out = os.path.join(ROOT, "ab", "wstamp")

@@ -28,6 +28,9 @@ L = ctypes.CDLL(LIB_PATH)
 st = np.zeros((3, 2048, 32), np.uint64)
 L.pst_x_wave_stamps(st.ctypes.data_as(ctypes.c_void_p))
 st = st.astype(np.int64)
+nst = np.zeros((3, 2048, 16), np.uint64)
+L.pst_x_node_stamps(nst.ctypes.data_as(ctypes.c_void_p))
+nst = nst.astype(np.int64)
 pct = lambda x: [round(float(v), 1) for v in np.percentile(x, [0, 10, 50, 90, 100])]
 for layer in range(3):
     w = st[layer]
@@ -46,5 +49,10 @@ for layer in range(3):
            "end_us": pct(us(w[:, 29] - t0))}
     simd = (w[:, 31] >> 4) & 3
     out["waves_per_simd_slot_check"] = int(len(np.unique(w[:, 31] & 0xffffffff)))
+    ns = nst[layer]
+    names = ["x_exchange", "ln0", "ffn_chunk0", "ffn_chunk1", "ffn_chunk2", "ffn_chunk3", "residual_exchange",
+             "ln1_store", "projections"]
+    out["node_phases_us_p10_50_90"] = {nm: [round(float(v), 1) for v in np.percentile(us(ns[:, k + 1] - ns[:, k]), [10, 50, 90])]
+                                       for k, nm in enumerate(names) if layer < 2 or nm != "projections"}
     print(json.dumps(out))
 tk.close()
