@@ -266,6 +266,7 @@ struct pst_ctx {
   int64_t half_tasks = -2;   // PST_HALF_TASKS: 1 = fused layers always two waves per task, 0 = never; -1 = policy
   int64_t mpnn_qwaves = -2;  // PST_MPNN_QWAVES: 4 = two 4-wave queue workgroups per CU; else one 8-wave workgroup
                              // per CU with all of W1 in LDS (k_mpnn<0..2> -1.0..-2.8 %, profiles/r04_ab_qwaves.txt)
+  int64_t pdb_gpu_max_file = -2;  // PST_PDB_GPU_MAX_FILE: bytes; a file this large sends the call to the host parser
   int64_t mpnn_qgroup = -2;  // PST_MPNN_QGROUP: queue unit order, tasks per group (0 = halves adjacent); -1 = wave slots per XCD
   int64_t mpnn_queue_layers = -2;  // PST_MPNN_QUEUE_LAYERS: layer mask of the queue form; -1 = MPNN_QUEUE_LAYERS
   int64_t mpnn_queue = -2;   // PST_MPNN_QUEUE: 1 = fused layers as the half-task queue (k_mpnn_q) whenever not
@@ -1321,9 +1322,15 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
     if (got != fsz[i]) bad_file.store(i);
   });
   if (bad_file.load() >= 0) return fail(ctx, PST_E_INVALID, std::string("cannot read ") + paths[bad_file.load()]);
+  // Files of 1 GB and more (offsets inside a file are 32-bit on the GPU path) send the whole
+  // call to the native host parser; PST_PDB_GPU_MAX_FILE lowers that bound (the GPU tests force
+  // the all-host route with it)
+  env_threshold(ctx->pdb_gpu_max_file, "PST_PDB_GPU_MAX_FILE");
+  const int64_t gpu_max = ctx->pdb_gpu_max_file >= 0 ? ctx->pdb_gpu_max_file : (int64_t)1 << 30;
+  const bool all_host = *std::max_element(fsz.begin(), fsz.end()) >= gpu_max;
   // ---- device scratch of the GPU parse (one grow-only allocation)
   pst::PdbScanArgs a{};
-  {
+  if (!all_host) {
     struct Item {
       void** p;
       size_t bytes;
@@ -1388,13 +1395,21 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
   for (int r = 0; r < 21; ++r)
     for (int q = 0; q < 37; ++q) a.tab.exists[r][q] = pst::kResAtomExists[r][q];
   hipStream_t st = ctx->stream;
-  HIPCHK(hipMemcpyAsync((void*)a.text, ctx->h_text, (size_t)T, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync((void*)a.file_off, foff.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync((void*)a.rec_base, rbase.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
-  pst::launch_pdb_scan(a, n, st);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(ctx->h_pdb_counts, a.n_res, sizeof(int32_t) * 3 * n, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  if (all_host) {
+    for (int i = 0; i < n; ++i) {
+      ctx->h_pdb_counts[i] = 0;
+      ctx->h_pdb_counts[n + i] = 0;
+      ctx->h_pdb_counts[2 * n + i] = 1;
+    }
+  } else {
+    HIPCHK(hipMemcpyAsync((void*)a.text, ctx->h_text, (size_t)T, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync((void*)a.file_off, foff.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync((void*)a.rec_base, rbase.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+    pst::launch_pdb_scan(a, n, st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(ctx->h_pdb_counts, a.n_res, sizeof(int32_t) * 3 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   const int32_t* g_res = ctx->h_pdb_counts;
   const int32_t* g_host = ctx->h_pdb_counts + 2 * n;
   // ---- the files outside the fast path: the native host parser (its results and its errors)
@@ -1443,9 +1458,11 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
   auto& w = ctx->w;
   a.pos = reinterpret_cast<float*>(w.pos);
   a.flags = w.flags;
-  HIPCHK(hipMemcpyAsync((void*)a.res_off, off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
-  pst::launch_pdb_write(a, n, st);
-  HIPCHK(hipGetLastError());
+  if (!all_host) {
+    HIPCHK(hipMemcpyAsync((void*)a.res_off, off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+    pst::launch_pdb_write(a, n, st);
+    HIPCHK(hipGetLastError());
+  }
   if (!host_ids.empty()) {  // host-parsed rows into their places (through the page-locked staging)
     const int64_t HR = hoff.back();
     if (HR > ctx->h_stage_cap) {

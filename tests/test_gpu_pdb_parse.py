@@ -62,6 +62,19 @@ def test_casp14_files_parsed_on_gpu_equal_host_parser(tk, casp):
     assert tk._pdb_tok.size >= 5618
 
 
+def test_large_files_send_the_call_to_the_host_parser(casp, monkeypatch):
+    """A file at or above the GPU path's size bound (1 GB: offsets inside a file are 32-bit on the
+    GPU) sends the whole call to the native host parser; PST_PDB_GPU_MAX_FILE lowers the bound so
+    the route runs here: every CASP14 file host-parsed, rows and tokens as the host parser's."""
+    from pst_amd._native import Tokenizer
+    monkeypatch.setenv("PST_PDB_GPU_MAX_FILE", "1000")
+    t = Tokenizer(0, 4096, 1, P.random_blob(6, 1234))
+    try:
+        _check_equal(t, casp, host_files=len(casp))
+    finally:
+        t.close()
+
+
 def _lines(path):
     with open(path) as fh:
         return fh.read().split("\n")
