@@ -667,8 +667,6 @@ __device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t
   }
 }
 
-template <int LAYER>
-__device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, int h, float* xs);
 
 // The edge phase of one fused-layer task (receivers task*32 .. task*32+31), edge blocks blk_lo ..
 // blk_hi-1 in order: edge update / embedding, message MLP, and the ordered segment sums of the
@@ -823,9 +821,10 @@ struct ClockStamp {
 // ordered segment sums in registers/LDS, then the node update. No per-edge message traffic.
 // HALF (batches of at most one round of tasks): two waves per task, wave 2t+h running edge
 // blocks 25h .. 25h+24 — exactly receivers 16h .. 16h+15 (800 = 16 x 50 edges), so each half's
-// segment sums are complete on their own; after a workgroup barrier wave 2t runs the node
-// update. The same operations in the same order: identical bits. Every SIMD then holds two
-// waves where a one-wave-per-task round would hold one.
+// segment sums are complete on their own; the wave that finishes its half second runs the
+// task's node update alone (an LDS counter per task; the first leaves). The same operations in
+// the same order: identical bits. Every SIMD then holds two waves where a one-wave-per-task round
+// would hold one.
 template <int LAYER, bool HALF>
 __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   __shared__ float lds_scratch[4][64 * 36];
@@ -840,12 +839,13 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   constexpr int KL = w1_lds_ksteps<LAYER>();
   __shared__ float4 w1_lds_buf[(KL > 0 ? KL : 1) * 64];
   const float4* w1_lds = KL > 0 ? w1_lds_buf : nullptr;
+  __shared__ int s_done[2];  // HALF: halves of each of the workgroup's two tasks finished
+  if (HALF && threadIdx.x < 2) s_done[threadIdx.x] = 0;
   if (KL > 0) {
     for (int i = threadIdx.x; i < KL * 64; i += 256) w1_lds_buf[i] = a.msg.w1[i];
-    __syncthreads();
   }
-  // HALF grids hold exactly n_tasks / 2 workgroups (n_tasks is a multiple of 4): no wave may
-  // leave before the barrier below
+  if (KL > 0 || HALF) __syncthreads();
+  // HALF grids hold exactly n_tasks / 2 workgroups (n_tasks is a multiple of 4)
   if (!HALF && task >= a.n_tasks) return;
   const int blk_lo = HALF ? 25 * hh : 0, blk_hi = HALF ? blk_lo + 25 : 50;
   const int64_t g0 = task * 32;
@@ -911,15 +911,22 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   // the sums were stored by other lanes of this wave (HALF: and by the partner wave): drain
   // stores, then read back
   if (HALF) {
+    // hand-off inside the workgroup: the wave that finishes its half FIRST leaves (its SIMD slot
+    // goes to the other workgroup's waves); the second runs the task's node update alone, the
+    // one-wave form below — so the later workgroup of a CU does not end the launch with node
+    // updates split over pairs of waves (round 5, per-wave stamps: those ran at half the MFMA
+    // rate, one wave per SIMD, after everything else)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_s_barrier();
+    int prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(&s_done[w >> 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev == 0) {
+      cs.stop(a.clk);
+      return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // the node update on both waves of the pair, two output blocks each, tiles exchanged
-    // through this pair's half of lds_scratch (free after the edge phase)
-    node_update_pair<LAYER>(a, g0, hh, lds_scratch[w & 2]);
-    cs.stop(a.clk);
-    return;
+    __builtin_amdgcn_s_waitcnt(0);
   } else {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_s_waitcnt(0);
@@ -1735,123 +1742,6 @@ __device__ __forceinline__ void blk_store_row(const f32x16& v, float* __restrict
   float4* p = reinterpret_cast<float4*>(row + (lane_id() >> 5) * 64 + w * 16);
 #pragma unroll
   for (int q = 0; q < 4; ++q) p[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-}
-
-// ------------------------------------------------------------- node_update_pair
-// k_mpnn<L, true>'s node update: wave h of the task's pair computes output blocks 2h and 2h+1 of
-// every GEMM (the block chains of k_mpnn_node_coop, same order, same bits); full tiles are
-// assembled through 16 KB of LDS, single-buffered (a barrier after the writes and after the
-// reads; every wave of the workgroup runs the same sequence).
-__device__ __forceinline__ void pair_exchange(Tile& t, const f32x16& p0, const f32x16& p1, float* xs, int h) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    xs[(2 * h * 16 + r) * 64 + lane] = p0[r];
-    xs[((2 * h + 1) * 16 + r) * 64 + lane] = p1[r];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int M = 0; M < 4; ++M)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) t.m[M][r] = xs[(M * 16 + r) * 64 + lane];
-  __syncthreads();
-}
-
-template <int LAYER>
-__device__ __forceinline__ void node_update_pair(const MpnnArgs& a, int64_t g0, int h, float* xs) {
-  const int lane = lane_id();
-  const int b0 = 2 * h, b1 = 2 * h + 1;
-  const int64_t gl = g0 + (lane & 31);
-  Tile x;
-  {
-    f32x16 ag0, ag1;
-    const float* b2 = a.msg.b2 + (lane >> 5) * 64;
-    const float fd = (float)a.deg[gl];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      ag0[r] = fd * b2[b0 * 16 + r];
-      ag1[r] = fd * b2[b1 * 16 + r];
-    }
-    {
-      Tile G;
-      tile_load_perm(G, a.agg + gl * 128);
-      blk_gemm(ag0, G, a.msg.w2, b0);
-      blk_gemm(ag1, G, a.msg.w2, b1);
-    }
-    const float* hrow;
-    if (LAYER == 0) {
-      const int lr = a.node_local[gl];
-      hrow = a.h0tab + (int64_t)(lr < 0 ? 0 : lr) * 128;
-    } else {
-      hrow = a.h_in + gl * 128;
-    }
-    f32x16 xp0 = blk_load_row(hrow, b0), xp1 = blk_load_row(hrow, b1);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      xp0[r] = xp0[r] + ag0[r] / 50.0f;
-      xp1[r] = xp1[r] + ag1[r] / 50.0f;
-    }
-    pair_exchange(x, xp0, xp1, xs, h);
-  }
-  tile_layer_norm(x, a.ln0_s, a.ln0_o);  // V_i_0
-  f32x16 out0, out1;
-  for (int ck = 0; ck < 4; ++ck) {
-    Tile hid;
-    {
-      f32x16 h0, h1;
-      blk_gemm_bf(h0, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, b0, ActId{});
-      blk_gemm_bf(h1, x, a.ff_w1 + ck * 64 * 64, a.ff_bf1 + ck * 64, b1, ActId{});
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f32x2 v0 = c_gelu2x((f32x2){h0[r], h0[r + 1]});
-        const f32x2 v1 = c_gelu2x((f32x2){h1[r], h1[r + 1]});
-        h0[r] = v0.x;
-        h0[r + 1] = v0.y;
-        h1[r] = v1.x;
-        h1[r + 1] = v1.y;
-      }
-      pair_exchange(hid, h0, h1, xs, h);
-    }
-    if (ck == 0) {
-      blk_gemm_bf(out0, hid, a.ff_w2, a.ff_bf2, b0, ActId{});
-      blk_gemm_bf(out1, hid, a.ff_w2, a.ff_bf2, b1, ActId{});
-    } else {
-      blk_gemm(out0, hid, a.ff_w2 + ck * 64 * 64, b0);
-      blk_gemm(out1, hid, a.ff_w2 + ck * 64 * 64, b1);
-    }
-  }
-  {
-    f32x16 xp0 = blk_pick(x, b0), xp1 = blk_pick(x, b1);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      xp0[r] = xp0[r] + out0[r];
-      xp1[r] = xp1[r] + out1[r];
-    }
-    pair_exchange(x, xp0, xp1, xs, h);
-  }
-  tile_layer_norm(x, a.ln1_s, a.ln1_o);  // V_i_1
-  blk_store_row(blk_pick(x, b0), a.h_out + gl * 128, b0);
-  blk_store_row(blk_pick(x, b1), a.h_out + gl * 128, b1);
-  if (a.P_out) {
-#pragma unroll 1
-    for (int p = 0; p < 4; ++p) {
-      f32x16 pr0, pr1;
-      if (p & 1) {
-        blk_gemm_bf(pr0, x, a.proj_w + p * 64 * 64, a.proj_bf[p >> 1], b0, ActId{});
-        blk_gemm_bf(pr1, x, a.proj_w + p * 64 * 64, a.proj_bf[p >> 1], b1, ActId{});
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          pr0[r] = 0.0f;
-          pr1[r] = 0.0f;
-        }
-        blk_gemm(pr0, x, a.proj_w + p * 64 * 64, b0);
-        blk_gemm(pr1, x, a.proj_w + p * 64 * 64, b1);
-      }
-      blk_store_row(pr0, a.P_out + gl * 512 + p * 128, b0);
-      blk_store_row(pr1, a.P_out + gl * 512 + p * 128, b1);
-    }
-  }
 }
 
 template <int LAYER>
