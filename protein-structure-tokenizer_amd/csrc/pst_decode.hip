@@ -1085,10 +1085,15 @@ __device__ __forceinline__ int ft_at(int C, int node, int c) { return node * ft_
 // acc[b] = X (16 nodes x K, LDS, optional ReLU on load) · W[:, 16·blk_b .. +15], blk_b = b0 + b·bstep.
 // Fully unrolled over K; the weight operands run PF groups of 4 k-steps (16 k) ahead in a register
 // ring (the weights are L2-resident: a fetch is ~1 us, ~4 groups of this wave's MFMAs).
+// prefetch depth in groups of 16 k (a build tunable: 8 and 12 measured no faster, fold stage 2.60 ms
+// either way; profiles/r05_ab_decode_ft_prefetch.txt)
+#ifndef FT_PF
+#define FT_PF 4
+#endif
 template <int NB, bool RELU_IN, int K>
 __device__ __forceinline__ void ft_gemm(f32x4t (&acc)[NB], const float* X, const float* __restrict__ W, int N,
                                         int b0, int bstep, int lane) {
-  constexpr int G = K / 16, PF = G < 4 ? G : 4;
+  constexpr int G = K / 16, PF = G < FT_PF ? G : FT_PF;
   const int node = lane & 15, j = lane >> 4;
   const float* xb = X + node * ft_sn(K) + j * ft_sj(K);
   int col[NB];
