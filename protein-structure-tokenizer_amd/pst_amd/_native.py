@@ -547,18 +547,20 @@ class Decoder:
         if nin is not None and nin.shape != (len(toks),):
             raise ValueError(f"{nin.shape} node counts for {len(toks)} proteins")
         n_total = int(off[-1]) * self.df if nin is None else int(nin.sum())
-        out = np.zeros((max(n_total, 1), 37, 3), np.float32)
+        # every row of every protein is written by the call (no zero fill needed); the results are
+        # disjoint views of these fresh arrays (no copies)
+        out = np.empty((max(n_total, 1), 37, 3), np.float32)
         nn = np.zeros(len(toks), np.int32)
-        up = np.zeros((max(int(off[-1]), 1), 128), np.float32) if with_up_proj else None
+        up = np.empty((max(int(off[-1]), 1), 128), np.float32) if with_up_proj else None
         self._check(lib().pst_decoder_decode_ex(self._h, _ptr(flat if flat.size else np.zeros(1, np.uint32)), _ptr(off),
                                                 len(toks), _ptr(nin), _ptr(out), _ptr(nn), _ptr(up)))
         res, o = [], 0
         for n in nn:
-            res.append(out[o:o + n].copy())
+            res.append(out[o:o + n])
             o += int(n)
         if not with_up_proj:
             return res
-        return res, [up[off[b]:off[b + 1]].copy() for b in range(len(toks))]
+        return res, [up[off[b]:off[b + 1]] for b in range(len(toks))]
 
     def debug(self, which: int, n_floats: int) -> np.ndarray:
         out = np.zeros(n_floats, np.float32)
