@@ -668,6 +668,18 @@ __device__ __forceinline__ void node_update(const MpnnArgs& a, int lane, int64_t
 }
 
 
+// Wave priority from the edge blocks a wave still has to run (s_setprio 3 / 2 / 1 / 0 while at
+// least 10 / 5 / 2 / 0 blocks of a 25-block half remain, `scale` x that for 50-block tasks). A
+// SIMD's two waves otherwise issue oldest-first: the older ran ahead and the younger finished the
+// launch alone at the one-wave rate. With the wave that has more left winning issue, the two end
+// together (same instructions, same bits; round 5, profiles/r05_ab_wave_priority.txt).
+__device__ __forceinline__ void tail_prio(int rem, int scale) {
+  if (rem >= 10 * scale) __builtin_amdgcn_s_setprio(3);
+  else if (rem >= 5 * scale) __builtin_amdgcn_s_setprio(2);
+  else if (rem >= 2 * scale) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 // The edge phase of one fused-layer task (receivers task*32 .. task*32+31), edge blocks blk_lo ..
 // blk_hi-1 in order: edge update / embedding, message MLP, and the ordered segment sums of the
 // receivers these blocks complete, stored to agg (perm rows). lds_scratch[w]: this wave's LDS tile.
@@ -682,6 +694,7 @@ __device__ __forceinline__ void mpnn_edge_blocks(const MpnnArgs& a, int64_t task
   int32_t s_next = edge_sender(a, g0, lane, blk_lo);
   for (int blk = blk_lo; blk < blk_hi; ++blk) {
     const int32_t s_cur = s_next;
+    tail_prio(blk_hi - blk, 1);
     if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
     edge_block<LAYER, KL>(a, task, g0, lane, blk, s_cur, m, w1_lds);
@@ -856,6 +869,8 @@ __global__ __launch_bounds__(256, MPNN_MIN_BLOCKS) void k_mpnn(MpnnArgs a) {
   int32_t s_next = edge_sender(a, g0, lane, blk_lo);
   for (int blk = blk_lo; blk < blk_hi; ++blk) {
     const int32_t s_cur = s_next;
+    if (HALF) tail_prio(blk_hi - blk, 1);
+    else tail_prio(blk_hi - blk, 2);
     if (blk < blk_hi - 1) s_next = edge_sender(a, g0, lane, blk + 1);
     Tile m;
     edge_block<LAYER>(a, task, g0, lane, blk, s_cur, m, w1_lds);

@@ -1,7 +1,7 @@
 """The N = 8 share of config 3 (128 x 256 residues) through the host-buffer path as bench.py runs it
 (float32 positions and flags in torch-pinned memory), calls 5 ms apart so a kernel + memory-copy
 trace separates them (tools/pdb_files_timeline.py prints the median call). PST_H2D_DENSE selects the
-wire format.   python tools/share_timeline_probe.py [--proteins 128] [--reps 10]"""
+wire format.   python tools/share_timeline_probe.py [--proteins 128] [--reps 10] [--save tokens.npy]"""
 import argparse
 import json
 import os
@@ -20,6 +20,7 @@ from pst_amd._native import Tokenizer, pack_samples  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--proteins", type=int, default=128)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--save", default="", help="np.save the tokens of the last call here")
 a = ap.parse_args()
 pos, flags, off = pack_samples(synthetic.synthetic_batch(a.proteins, 256, seed=1000))
 ppos = torch.from_numpy(pos.astype(np.float32)).pin_memory().numpy()
@@ -31,8 +32,10 @@ ts = []
 for _ in range(a.reps):
     time.sleep(0.005)
     t0 = time.perf_counter()
-    tk.tokenize_packed(ppos, pflags, off)
+    res = tk.tokenize_packed(ppos, pflags, off)
     ts.append(time.perf_counter() - t0)
+if a.save:
+    np.save(a.save, res[0])
 print(json.dumps({"proteins": a.proteins, "ms_median": round(float(np.median(ts)) * 1e3, 3),
                   "dense": os.environ.get("PST_H2D_DENSE", "policy")}))
 tk.close()
