@@ -1327,8 +1327,9 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
   // the all-host route with it)
   env_threshold(ctx->pdb_gpu_max_file, "PST_PDB_GPU_MAX_FILE");
   const int64_t gpu_max = ctx->pdb_gpu_max_file >= 0 ? ctx->pdb_gpu_max_file : (int64_t)1 << 30;
-  const bool all_host = *std::max_element(fsz.begin(), fsz.end()) >= gpu_max;
-  // ---- device scratch of the GPU parse (one grow-only allocation)
+  bool all_host = *std::max_element(fsz.begin(), fsz.end()) >= gpu_max;
+  // ---- device scratch of the GPU parse (one grow-only allocation, about 10x the text: when it
+  // cannot be had, the whole call takes the native host parser instead of failing)
   pst::PdbScanArgs a{};
   if (!all_host) {
     struct Item {
@@ -1360,17 +1361,23 @@ int pst_tokenize_pdb_files(pst_ctx* ctx, const char* const* paths, int32_t n, in
       if (ctx->d_pdb) (void)hipFree(ctx->d_pdb);
       ctx->d_pdb = nullptr;
       ctx->d_pdb_cap = 0;
-      hipError_t e = hipMalloc(&ctx->d_pdb, total);
-      if (e != hipSuccess) return fail(ctx, PST_E_NOMEM, std::string("PDB parse scratch: ") + hipGetErrorString(e));
-      ctx->d_pdb_cap = total;
+      if (hipMalloc(&ctx->d_pdb, total) != hipSuccess) {
+        (void)hipGetLastError();  // clear the sticky error: the host route follows
+        ctx->d_pdb = nullptr;
+        all_host = true;
+      } else {
+        ctx->d_pdb_cap = total;
+      }
     }
-    char* q = (char*)ctx->d_pdb;
-    for (const auto& it : items) {
-      *it.p = q;
-      q += (it.bytes + 255) / 256 * 256;
+    if (!all_host) {
+      char* q = (char*)ctx->d_pdb;
+      for (const auto& it : items) {
+        *it.p = q;
+        q += (it.bytes + 255) / 256 * 256;
+      }
+      a.n_run = a.n_res + n;
+      a.host_path = a.n_res + 2 * n;
     }
-    a.n_run = a.n_res + n;
-    a.host_path = a.n_res + 2 * n;
   }
   if (3 * (int64_t)n > ctx->h_pdb_counts_cap) {
     if (ctx->h_pdb_counts) (void)hipHostFree(ctx->h_pdb_counts);

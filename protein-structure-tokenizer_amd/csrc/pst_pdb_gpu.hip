@@ -24,7 +24,7 @@
 //     outside atom37 are dropped; residues without an atom37 atom are skipped; the residue type
 //     is the first record's resname among the 20 standard ones, else UNK.
 // Every choice above is checked against the host parser bit for bit on the GPU
-// (tests/test_gpu_cli.py: positions and flags of every CASP14 file and of handcrafted files
+// (tests/test_gpu_pdb_parse.py: positions and flags of every CASP14 file and of handcrafted files
 // covering each host-path trigger).
 #include "pst_kernels.h"
 
@@ -235,6 +235,17 @@ __global__ __launch_bounds__(PDB_THREADS) void k_pdb_scan(PdbScanArgs a) {
   const int n_lines = at;  // separators + 1 (the last line may be empty)
   __syncthreads();
   const int start = s_start;
+  if (start == PDB_INT_MAX) {
+    // no ATOM / HETATM / MODEL line (empty, header-only or REMARK/TER-only file): the native
+    // parser raises the reference's error for it (pst_pdb.cpp, "Found 0 models"). Uniform exit:
+    // start is the same LDS value in every thread and no barrier follows.
+    if (tid == 0) {
+      a.n_res[f] = 0;
+      a.n_run[f] = 0;
+      a.host_path[f] = 1;
+    }
+    return;
+  }
   for (int i = tid; i < n_lines; i += PDB_THREADS)
     if (i > start && a.line_kind[lb + i] == K_STOP) atomicMin(&s_stop, i);
   __syncthreads();

@@ -142,7 +142,7 @@ def test_fast_path_variants_and_host_path_triggers(tk, casp, tmp_path):
 
 def test_host_path_errors_are_the_host_parsers(tk, casp, tmp_path):
     """Errors come from the host parser with its messages: two models, an insertion code, a
-    missing file."""
+    missing file (files without coordinates: the test below)."""
     from pst_amd._native import PstError
     base = _lines(casp[2])
     atoms = [i for i, l in enumerate(base) if l.startswith("ATOM  ")]
@@ -158,4 +158,25 @@ def test_host_path_errors_are_the_host_parsers(tk, casp, tmp_path):
     with pytest.raises(ValueError, match="cannot open"):
         tk.tokenize_pdb_files([casp[0], str(tmp_path / "missing.pdb")])
     # the context keeps working after the errors
+    _check_equal(tk, casp[:3], host_files=0)
+
+
+@pytest.mark.parametrize("kind", ["empty", "header", "remark_ter", "crlf_header"])
+def test_files_without_coordinates_take_the_host_parsers_error(tk, casp, tmp_path, kind):
+    """A file with no ATOM / HETATM / MODEL line (empty, header-only, REMARK/TER-only) has no
+    coordinate section: the GPU scan hands it to the host parser, whose error is the reference's
+    ("Found 0 models", protein_structure_sample.py:166-248 via Bio's empty structure), alone and
+    beside GPU-path files; the context stays usable afterwards."""
+    base = _lines(casp[0])
+    header = [l for l in base[:40] if not l.startswith(("ATOM", "HETATM", "MODEL"))]
+    body = {"empty": [], "header": header, "remark_ter": ["REMARK   1 NOTHING HERE", "TER", "END"],
+            "crlf_header": header}[kind]
+    path = _write(tmp_path, f"{kind}.pdb", body, nl="\r\n" if kind == "crlf_header" else "\n")
+    with pytest.raises(ValueError) as host_err:
+        _host([path]).sample(0)
+    for paths in ([path], [casp[0], path, casp[1]]):
+        with pytest.raises(Exception) as gpu_err:
+            tk.tokenize_pdb_files(paths)
+        assert "Found 0 models" in str(gpu_err.value)
+    assert "Found 0 models" in str(host_err.value)
     _check_equal(tk, casp[:3], host_files=0)
