@@ -518,11 +518,9 @@ __global__ void k_affine_init(float* __restrict__ aff, float* __restrict__ rot, 
 }
 
 // QuatAffine.pre_compose (quat_affine.py:288-317): q += q ⊗ (0, v); t += R·dt; renormalise
-__device__ __forceinline__ void affine_update(float* __restrict__ aff, float* __restrict__ rot,
-                                              const float* __restrict__ upd, int i) {
+__device__ __forceinline__ void affine_update(float* __restrict__ aff, float* __restrict__ rot, const float* u, int i) {
   float* a = aff + i * 7;
   float* R = rot + i * 9;
-  const float* u = upd + i * 6;
   const float q0 = a[0], q1 = a[1], q2 = a[2], q3 = a[3];
   const float v1 = u[0], v2 = u[1], v3 = u[2];
   float nq[4];
@@ -586,7 +584,7 @@ __global__ void k_ipa_points(const float* __restrict__ qpl /*[N][144]*/, const f
 // a k-ascending fmaf chain (tools/probe/mfma_probe.hip: 256/256 bitwise), so every sum is the
 // in-order chain over j from 0 (round 3 measured it bitwise equal to per-query VALU fmaf chains;
 // that form is tools/variants/decode_ab.patch). The attention weights go to att_out for the
-// value sums (k_ipa_values) and the local frames (k_ipa_local).
+// value sums and the local frames (k_ipa_values).
 constexpr int ATT_LD = 13;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -725,13 +723,17 @@ __global__ __launch_bounds__(256) void k_ipa_attn(const float* __restrict__ qs /
 // D[q][o] = Σ_j att[q][h][j] · V_h[j][o] on v_mfma_f32_16x16x4_f32 for the 16 scalar values and
 // the 8 value points × xyz (24) of head h — three 16-wide output blocks (8 columns unused). The
 // instruction is a k-ascending fmaf chain, so each sum is the in-order chain over j from 0 that
-// a per-query VALU loop would run: identical bits. Scalar outputs go to feat[q][16h + o], the
-// global-frame points to vpt[q][24h + o'] for k_ipa_local.
+// a per-query VALU loop would run: identical bits. Scalar outputs go to feat[q][16h + o]. The
+// global-frame value points then go to each query's local frame (invert_point) with their norms
+// (folding.py:256-275) in this launch (round 6; they were the separate k_ipa_local launch, through
+// a [N][288] buffer): the 16 x 24 point coordinates through LDS, two (query, point) pairs per lane,
+// the same operations in the same order as before.
 __global__ __launch_bounds__(64) void k_ipa_values(const float* __restrict__ att_all, const float* __restrict__ kvs_all,
                                                    const float* __restrict__ kvpg_all, float* __restrict__ feat,
-                                                   float* __restrict__ vpt, DecBatch bt,
-                                                   const int32_t* __restrict__ vt_prot,
+                                                   const float* __restrict__ aff, const float* __restrict__ rot,
+                                                   DecBatch bt, const int32_t* __restrict__ vt_prot,
                                                    const int32_t* __restrict__ vt_q0, int ld) {
+  __shared__ float sp[16][25];  // [query][point coordinate o = 3p + xyz] (+1 pad)
   const int tile = blockIdx.x, h = blockIdx.y;
   const int lane = threadIdx.x, i = lane & 15, g = lane >> 4;
   const int b = vt_prot[tile], q0 = vt_q0[tile];
@@ -766,53 +768,50 @@ __global__ __launch_bounds__(64) void k_ipa_values(const float* __restrict__ att
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int q = q0 + 4 * g + r;
-    if (q >= N) continue;
-    const int64_t row = n0 + q;
-    feat[row * 2112 + h * 16 + i] = acc0[r];
-    vpt[row * 288 + h * 24 + i] = acc1[r];
-    if (i < 8) vpt[row * 288 + h * 24 + 16 + i] = acc2[r];
+    const int q = 4 * g + r;
+    sp[q][i] = acc1[r];
+    if (i < 8) sp[q][16 + i] = acc2[r];
+    if (q0 + q >= N) continue;
+    feat[(n0 + q0 + q) * 2112 + h * 16 + i] = acc0[r];
   }
-}
-
-// Value points of query i from the global frame to its local frame (invert_point) and their norms
-// (folding.py:256-275), after k_ipa_values.
-__global__ void k_ipa_local(const float* __restrict__ vpt, const float* __restrict__ aff,
-                            const float* __restrict__ rot, float* __restrict__ feat, int N) {
-  const int64_t ig = blockIdx.x;
-  const int tid = threadIdx.x;  // 96
-  if (ig >= N) return;
-  const float* res_pt = vpt + ig * 288;
-  float* f = feat + ig * 2112;
-  const int h = tid / 8, p = tid % 8;
-  const float* R = rot + ig * 9;
-  const float* tr = aff + ig * 7 + 4;
-  const float gx = res_pt[(h * 8 + p) * 3 + 0] - tr[0];
-  const float gy = res_pt[(h * 8 + p) * 3 + 1] - tr[1];
-  const float gz = res_pt[(h * 8 + p) * 3 + 2] - tr[2];
-  const float lx = R[0] * gx + R[3] * gy + R[6] * gz;
-  const float ly = R[1] * gx + R[4] * gy + R[7] * gz;
-  const float lz = R[2] * gx + R[5] * gy + R[8] * gz;
-  f[192 + tid] = lx;
-  f[288 + tid] = ly;
-  f[384 + tid] = lz;
-  f[480 + tid] = sqrtf(((1e-8f + lx * lx) + ly * ly) + lz * lz);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int e = lane + 64 * k, q = e >> 3, p = e & 7;
+    if (q0 + q >= N) continue;
+    const int64_t ig = n0 + q0 + q;
+    const float* R = rot + ig * 9;
+    const float* tr = aff + ig * 7 + 4;
+    const float gx = sp[q][3 * p + 0] - tr[0];
+    const float gy = sp[q][3 * p + 1] - tr[1];
+    const float gz = sp[q][3 * p + 2] - tr[2];
+    const float lx = R[0] * gx + R[3] * gy + R[6] * gz;
+    const float ly = R[1] * gx + R[4] * gy + R[7] * gz;
+    const float lz = R[2] * gx + R[5] * gy + R[8] * gz;
+    float* f = feat + ig * 2112;
+    const int c = h * 8 + p;
+    f[192 + c] = lx;
+    f[288 + c] = ly;
+    f[384 + c] = lz;
+    f[480 + c] = sqrtf(((1e-8f + lx * lx) + ly * ly) + lz * lz);
+  }
 }
 
 // Backbone torsions → frames → atom14 → atom37 (folding.py:674-746, all_atom.py:473-595, :122-135)
 // plus the trajectory row (affine × [1,1,1,1,10,10,10]).
-__global__ void k_sc_geom(float* __restrict__ aff, float* __restrict__ rot, const float* __restrict__ upd /*[N][6]*/,
-                          const float* __restrict__ unnorm /*[N][6]*/, float* __restrict__ angles /*[N][3][2]*/,
-                          float* __restrict__ traj /*[N][7]*/, float* __restrict__ atom37 /*[N][37][3] or null*/,
-                          float* __restrict__ atom14 /*[N][14][3] or null*/, int N) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  affine_update(aff, rot, upd, i);  // this iteration's backbone update first (was k_affine_update)
+// One node i: this iteration's backbone update (affine_update, from the 6 update values `u6`), then
+// the torsions (the 6 unnormalised sin / cos values `un6`), trajectory row and, on the last
+// iteration, the atoms. Runs at the end of k_fold_tail (round 6; it was the k_sc_geom launch).
+__device__ void sc_geom_node(float* __restrict__ aff, float* __restrict__ rot, const float* u6, const float* un6,
+                             float* __restrict__ angles /*[N][3][2]*/, float* __restrict__ traj /*[N][7]*/,
+                             float* __restrict__ atom37 /*[N][37][3] or null*/,
+                             float* __restrict__ atom14 /*[N][14][3] or null*/, int i) {
+  affine_update(aff, rot, u6, i);
   const float* a = aff + i * 7;
   const float* R = rot + i * 9;
   float sn[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {1.f, 1.f, 1.f, 1.f};
   for (int t = 0; t < 3; ++t) {
-    const float s = unnorm[i * 6 + 2 * t], c = unnorm[i * 6 + 2 * t + 1];
+    const float s = un6[2 * t], c = un6[2 * t + 1];
     const float d = sqrtf(fmaxf(s * s + c * c, 1e-12f));
     sn[t + 1] = s / d;
     cs[t + 1] = c / d;
@@ -1075,6 +1074,8 @@ struct FoldTailArgs {
   const float *w_sc, *b_sc, *w_sc1, *b_sc1;
   const float *w_rb[4], *b_rb[4];  // rb1, rb2, rb1_1, rb2_1
   const float *w_ang, *b_ang;
+  // the iteration's geometry (sc_geom_node) for the tile's nodes after the angles
+  float *aff, *rot, *angles, *traj, *atom37, *atom14;
 };
 
 // strides of a [16 nodes][C] LDS activation (C = 384 or 128): plane j = k & 3 of node n starts at
@@ -1146,14 +1147,19 @@ __device__ __forceinline__ void ft_store(const f32x4t (&acc)[NB], float* Y, int 
     }
 }
 
-// the same epilogue for a 6-wide output (one block, wave 0) straight to global rows [N][6]
-__device__ __forceinline__ void ft_store6(const f32x4t& acc, float* __restrict__ out, const float* __restrict__ bias,
-                                          int64_t node0, int N, int lane) {
+// the same epilogue for a 6-wide output (one block, wave 0) to global rows [N][6] and the tile's
+// LDS copy [16][6]
+__device__ __forceinline__ void ft_store6(const f32x4t& acc, float* __restrict__ out, float* lds,
+                                          const float* __restrict__ bias, int64_t node0, int N, int lane) {
   const int64_t node = node0 + (lane & 15);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int n = 4 * (lane >> 4) + r;
-    if (n < 6 && node < N) out[node * 6 + n] = acc[r] + bias[n];
+    if (n < 6) {
+      const float v = acc[r] + bias[n];
+      lds[(lane & 15) * 6 + n] = v;
+      if (node < N) out[node * 6 + n] = v;
+    }
   }
 }
 
@@ -1305,6 +1311,7 @@ __global__ __launch_bounds__(64 * FT_WAVES) void k_fold_tail(FoldTailArgs a) {
   __shared__ __attribute__((aligned(16))) float S0[FT_NODES * ft_sn(128)];
   __shared__ __attribute__((aligned(16))) float S1[FT_NODES * ft_sn(128)];
   __shared__ __attribute__((aligned(16))) float IR[FT_NODES * ft_sn(128)];
+  __shared__ float UPD[FT_NODES * 6], UN[FT_NODES * 6];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // FT_WAVES waves
   const int64_t node0 = (int64_t)blockIdx.x * FT_NODES;
@@ -1342,7 +1349,7 @@ __global__ __launch_bounds__(64 * FT_WAVES) void k_fold_tail(FoldTailArgs a) {
     f32x4t acc[1], acc2[1];
     if (w == 8) {  // backbone affine update (6 outputs)
       ft_gemm<1, false, 384>(acc, A0, a.w_aff, 6, 0, 1, lane);
-      ft_store6(acc[0], a.upd, a.b_aff, node0, a.N, lane);
+      ft_store6(acc[0], a.upd, UPD, a.b_aff, node0, a.N, lane);
     }
     // sidechain input: sc_in(relu(act)) + sc_in1(relu(init_act)), wave w owns block w of 8
     if (w < 8) {
@@ -1371,9 +1378,13 @@ __global__ __launch_bounds__(64 * FT_WAVES) void k_fold_tail(FoldTailArgs a) {
     }
     if (w == 0) {  // torsion angles (unnormalised, 6 outputs)
       ft_gemm<1, true, 128>(acc, S0, a.w_ang, 6, 0, 1, lane);
-      ft_store6(acc[0], a.unnorm, a.b_ang, node0, a.N, lane);
+      ft_store6(acc[0], a.unnorm, UN, a.b_ang, node0, a.N, lane);
     }
   }
+  __syncthreads();
+  if (threadIdx.x < FT_NODES && node0 + threadIdx.x < a.N)
+    sc_geom_node(a.aff, a.rot, UPD + threadIdx.x * 6, UN + threadIdx.x * 6, a.angles, a.traj, a.atom37, a.atom14,
+                 (int)(node0 + threadIdx.x));
 }
 
 __global__ __launch_bounds__(256) void k_relu_copy(const float* __restrict__ X, int ldx, float* __restrict__ Y,
@@ -1438,7 +1449,7 @@ struct Scratch {
   float *aff, *rot, *unnorm, *angles, *traj, *atom37, *atom14, *kT, *kpT, *init_relu, *ipa_in;
   int64_t *tok_off, *node_off, *pair_off;
   int32_t *tok_prot, *node_prot, *vt_prot, *vt_q0;
-  float *att, *vpt;
+  float *att;
   uint32_t* tokens;
 };
 
@@ -1467,7 +1478,7 @@ int ensure_ws(pst_decoder* dec, Scratch* S) {
                 {(void**)&S->pair_off, (NN + 1) * sizeof(int64_t)}, {(void**)&S->tok_prot, NN * sizeof(int32_t)},
                 {(void**)&S->node_prot, NN * sizeof(int32_t)}, {(void**)&S->tokens, NN * sizeof(uint32_t)},
                 {(void**)&S->vt_prot, 2 * NN * sizeof(int32_t)}, {(void**)&S->vt_q0, 2 * NN * sizeof(int32_t)},
-                {(void**)&S->att, NP * 12 * F}, {(void**)&S->vpt, NN * 288 * F}};
+                {(void**)&S->att, NP * 12 * F}};
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 255) / 256 * 256;
   if (!dec->ws) {
@@ -1608,21 +1619,18 @@ int decode_group(pst_decoder* dec, Scratch& S, const Group& G, bool keep_debug) 
                          S.kvs, S.kT, S.kpT, Ni, 1152);
       hipLaunchKernelGGL(k_ipa_attn, dim3((unsigned)N), dim3(256), 0, st, S.qs, S.qpg, S.b2d, S.zln,
                          dec->d_pw, S.aff, S.rot, S.feat, bt, S.kT, S.kpT, Ni, 1152, S.att);
-      hipLaunchKernelGGL(k_ipa_values, dim3((unsigned)n_vt, 12), dim3(64), 0, st, S.att, S.kvs, S.kvpg, S.feat, S.vpt,
-                         bt, S.vt_prot, S.vt_q0, 1152);
-      hipLaunchKernelGGL(k_ipa_local, dim3((unsigned)N), dim3(96), 0, st, S.vpt, S.aff, S.rot, S.feat, Ni);
+      hipLaunchKernelGGL(k_ipa_values, dim3((unsigned)n_vt, 12), dim3(64), 0, st, S.att, S.kvs, S.kvpg, S.feat, S.aff,
+                         S.rot, bt, S.vt_prot, S.vt_q0, 1152);
       gemm(st, S.feat, 2112, W.out_proj, S.act, 384, Ni, F_ACCUM);  // act += IPA
       // the rest of the iteration's linears and norms in one launch (k_fold_tail)
+      const bool last = it == 7;
       FoldTailArgs ft{S.act, S.init_relu, S.upd, S.unnorm, Ni, W.att_ln.s, W.att_ln.o, W.tr_ln.s, W.tr_ln.o,
                       {W.tr[0].w, W.tr[1].w, W.tr[2].w}, {W.tr[0].b, W.tr[1].b, W.tr[2].b},
                       W.affine_update.w, W.affine_update.b, W.sc_in.w, W.sc_in.b, W.sc_in1.w, W.sc_in1.b,
                       {W.rb1.w, W.rb2.w, W.rb1_1.w, W.rb2_1.w}, {W.rb1.b, W.rb2.b, W.rb1_1.b, W.rb2_1.b},
-                      W.angles.w, W.angles.b};
+                      W.angles.w, W.angles.b, S.aff, S.rot, S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7,
+                      last ? S.atom37 : nullptr, last ? S.atom14 : nullptr};
       hipLaunchKernelGGL(k_fold_tail, dim3((unsigned)((N + FT_NODES - 1) / FT_NODES)), dim3(64 * FT_WAVES), 0, st, ft);
-      const bool last = it == 7;
-      hipLaunchKernelGGL(k_sc_geom, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, S.aff, S.rot, S.upd, S.unnorm,
-                         S.angles + it * kNodeCap * 6, S.traj + it * kNodeCap * 7, last ? S.atom37 : nullptr,
-                         last ? S.atom14 : nullptr, Ni);
     }
     mark(4);
     DCHK(hipGetLastError());

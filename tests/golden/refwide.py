@@ -17,6 +17,12 @@ PATH = os.path.join(HERE, "forward_ref_wide.npz")
 # the headline workload pinned to the reference (make_forward_bench.py + compact_bench.py): every
 # protein of bench.py's config-3 workload (bench256) and every 16th of config 5's (bench512)
 BENCH_PATH = os.path.join(HERE, "forward_ref_bench.npz")
+# the 31 CASP14 structures at (codebook, df) = (4096, 2), (4096, 4), (64000, 2), (64000, 4): the
+# reference CLI's other --model_downsampling settings (make_forward_casp_df.py); inputs are the
+# rows of casp14_atom37.npz
+CASP_DF_PATH = os.path.join(HERE, "forward_ref_casp_df.npz")
+CASP_PATH = os.path.join(HERE, "casp14_atom37.npz")
+CASP_DF_CONFIGS = [(4096, 2), (4096, 4), (64000, 2), (64000, 4)]
 # tokens whose reference margin is below CLOSE keep their bounded latent in the compact fixture
 CLOSE = 1e-4
 # The headline workload's tokens that a float32 implementation resolves to the other side of a
@@ -29,6 +35,9 @@ KNOWN_BOUNDARY_CASES = {("bench256", 924, 3): 5}
 # computation in PyTorch-CPU float32, on every 16th protein): its float32 sums flip the workload's
 # closest token (margin 8.8e-8), which the GPU path resolves as the reference does.
 KNOWN_CPU_BASELINE_CASES = {("bench256", 352, 221): 2}
+# The same list for the CASP14 downsampling fixture: (case, token) -> dim. Measured on all 124 cases
+# (oracle = GPU bits); an unlisted flip, or a listed one that no longer flips, fails.
+KNOWN_CASP_DF_CASES = {}
 # log10 bins of the margin histogram: [0, 1e-7), [1e-7, 1e-6), ..., [1e-1, 0.5]
 EDGES = [0.0, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2, 1e-1, 0.5000001]
 
@@ -234,3 +243,63 @@ class BenchSample:
 
 def load_bench_sample(name="bench256", F=None):
     return BenchSample(F if F is not None else load_bench(), name)
+
+
+def load_casp_df():
+    return np.load(CASP_DF_PATH)
+
+
+def casp_df_cases(F, cb, df):
+    """The fixture's cases of one (codebook, df), in casp14_atom37.npz order."""
+    C = np.load(CASP_PATH)
+    names = [f"casp_{str(n)}_k{cb}_df{df}" for n in C["names"]]
+    return [c for c in names if c + "/tokens" in F.files]
+
+
+def casp_inputs(case):
+    """(positions f32 [n,37,3], flags u8 [n,37]) of a casp_{name}_k.._df.. case."""
+    C = np.load(CASP_PATH)
+    nm = case.split("_")[1]
+    i = [str(x) for x in C["names"]].index(nm)
+    a, b = int(C["offsets"][i]), int(C["offsets"][i + 1])
+    return C["positions"][a:b], C["flags"][a:b]
+
+
+def compare_cases(F, outs, known=None):
+    """Token ids (and bounded latents) of each case vs the reference fixture F (keys tokens /
+    bounded / margin / meta): `outs` = {case: (tokens, bounded)}. Lists every mismatch with its
+    reference margin, the dim whose rounding differs and our deviation there; `unexplained` = a
+    mismatch whose margin is not below our deviation (a real error), `unlisted` = a flip missing
+    from `known` (KNOWN_CASP_DF_CASES by default), `missing_known` = a listed case that did not flip."""
+    known = KNOWN_CASP_DF_CASES if known is None else known
+    n_tok = n_eq = 0
+    mism, unexplained, unlisted, reps = [], [], [], []
+    max_dev = 0.0
+    for c, (tok, b) in outs.items():
+        ref_t = np.asarray(F[c + "/tokens"])
+        ref_b = np.asarray(F[c + "/bounded"], np.float64)
+        tok = np.asarray(tok)[:len(ref_t)]
+        b = np.asarray(b, np.float64)[:len(ref_t)]
+        if len(tok) != len(ref_t):
+            raise AssertionError(f"{c}: {len(tok)} tokens vs reference {len(ref_t)}")
+        dm = dim_margins(ref_b)
+        dev = np.abs(b - ref_b[:, :b.shape[1]])
+        max_dev = max(max_dev, float(dev.max()) if dev.size else 0.0)
+        reps.append(report(ref_b, ref_t, b, tok))
+        n_tok += len(ref_t)
+        bad = np.nonzero(tok != ref_t)[0]
+        n_eq += len(ref_t) - len(bad)
+        for t in bad:
+            d = int(np.argmin(dm[t]))
+            rec = {"case": c, "token": int(t), "ref_token": int(ref_t[t]), "our_token": int(tok[t]),
+                   "ref_margin": float(dm[t].min()), "dim": d, "our_deviation": float(dev[t, d])}
+            (mism if rec["our_deviation"] > rec["ref_margin"] else unexplained).append(rec)
+            if known.get((c, int(t))) != d:
+                unlisted.append(rec)
+    flipped = {(r["case"], r["token"]) for r in mism + unexplained}
+    missing = [list(k) for k in known if k[0] in outs and k not in flipped]
+    r = merge(reps) if reps else {}
+    r.update({"cases": len(outs), "tokens": n_tok, "identical": n_eq, "max_deviation": max_dev,
+              "mismatches": mism + unexplained, "unexplained": unexplained, "unlisted": unlisted,
+              "missing_known": missing})
+    return r

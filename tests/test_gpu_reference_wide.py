@@ -106,3 +106,36 @@ def test_gpu_tokens_equal_reference_config5_sample():
     r = _run_bench_sample(S, 64000, 4)
     print({k: r[k] for k in ("tokens", "identical", "min_margin", "close_tokens", "max_deviation_close")})
     assert r["tokens"] == 4096 and r["identical"] == r["tokens"], r
+
+
+@pytest.mark.parametrize("cb,df", refwide.CASP_DF_CONFIGS)
+def test_gpu_tokens_equal_reference_casp_df(cb, df):
+    """The 31 CASP14 structures in ONE ragged batch per (codebook, df) at the reference CLI's other
+    downsampling settings (df 2 and df 4: the local-window cross-attention downsampler, model.py:
+    264-318, modules.py:427-534) through the C ABI, against the reference's forward (_pe32 rendering,
+    forward_ref_casp_df.npz): every token identical except the listed boundary cases
+    (refwide.KNOWN_CASP_DF_CASES); an unlisted flip or a listed case that no longer flips fails."""
+    from pst_amd._native import pack_samples  # noqa: F401  (same binding as the other tests)
+    G = refwide.load_casp_df()
+    cases = refwide.casp_df_cases(G, cb, df)
+    assert len(cases) == 31
+    ins = [refwide.casp_inputs(c) for c in cases]
+    pos = np.concatenate([p for p, _ in ins]).astype(np.float32)
+    fl = np.concatenate([f for _, f in ins])
+    off = np.zeros(len(cases) + 1, np.int64)
+    off[1:] = np.cumsum([p.shape[0] for p, _ in ins])
+    D, seed = (int(v) for v in G[cases[0] + "/meta"][4:6])
+    tk = _make(cb, df, D, seed)
+    tok, nt, nn = tk.tokenize_packed(pos, fl, off)
+    b = tk.aux(int(off[-1]))["bounded"]
+    tk.close()
+    outs = {}
+    for i, c in enumerate(cases):
+        n, T = (int(v) for v in G[c + "/meta"][:2])
+        assert int(nn[i]) == n and int(nt[i]) == T, c
+        a = int(off[i])
+        outs[c] = (tok[a:a + T].copy(), b[a:a + T].copy())
+    r = refwide.compare_cases(G, outs)
+    print({k: r[k] for k in ("cases", "tokens", "identical", "min_margin", "max_deviation", "mismatches")})
+    assert not r["unexplained"] and not r["unlisted"] and not r["missing_known"], r
+    assert r["max_deviation"] < TOL["_pe32"][1]

@@ -154,3 +154,30 @@ def test_oracle_tokens_equal_reference_config5_sample():
     r = _oracle_sample(S, [int(p) for p in S.proteins], LEVELS[64000], 4)
     print({k: r[k] for k in ("tokens", "identical", "min_margin", "close_tokens", "max_deviation_close")})
     assert r["tokens"] == 4096 and r["identical"] == 4096, r
+
+
+# ------------------------------------------------------------ CASP14 at df 2 / df 4
+# forward_ref_casp_df.npz (golden/make_forward_casp_df.py): the reference's forward (_pe32 rendering)
+# on all 31 CASP14 structures at the reference CLI's other downsampling settings — (4096, df 2),
+# (4096, df 4), (64000, df 2), (64000, df 4) — which run the local-window cross-attention
+# downsampler and its pooling (model.py:264-318, modules.py:427-534) that df 1 does not.
+@pytest.mark.parametrize("cb,df", refwide.CASP_DF_CONFIGS)
+def test_oracle_tokens_equal_reference_casp_df(cb, df):
+    G = refwide.load_casp_df()
+    cases = refwide.casp_df_cases(G, cb, df)
+    assert len(cases) == 31
+
+    def run(c):
+        pos, fl = refwide.casp_inputs(c)
+        n, T, mcb, mdf, D, seed = (int(v) for v in G[c + "/meta"])
+        assert (mcb, mdf) == (cb, df)
+        o = O.tokenize(P.random_blob(D, seed), LEVELS[cb], df, pos.astype(np.float64), fl)
+        assert o["graph"]["n"] == n and len(o["tokens"]) == T, c
+        return c, (o["tokens"], o["b"])
+
+    with ThreadPoolExecutor(8) as ex:
+        outs = dict(ex.map(run, cases))
+    r = refwide.compare_cases(G, outs)
+    print({k: r[k] for k in ("cases", "tokens", "identical", "min_margin", "max_deviation", "mismatches")})
+    assert not r["unexplained"] and not r["unlisted"] and not r["missing_known"], r
+    assert r["max_deviation"] < TOL["_pe32"][1]

@@ -41,6 +41,11 @@ N = a.tokens * a.df
 # (pst_decode.hip k_pair_fused: 13 K=128 tile GEMMs x 256 — out1 x4, out2 x2, right1 x2, seq_linear,
 # pt1 x2, pt2 x2 — + 2 bias k-step groups x 4 + the 64-step narrow attention-bias GEMM = 3 400)
 MFMA_PER_PAIR_TILE = 13 * 256 + 2 * 4 + 64
+# launches per fold iteration (pst_decode.hip decode_group): the 384 -> 1152 IPA input GEMM,
+# k_ipa_points, k_ipa_attn, k_ipa_values (+ the local frames, round 6), the 2112 -> 384 output
+# projection GEMM, k_fold_tail (+ the backbone update and geometry, round 6); 8 before round 6
+FOLD_LAUNCHES_PER_ITERATION = 6
+FOLD_ITERATIONS = 8
 PEAK_FP32_TFLOPS = 157.3
 dec.set_timing(True)
 for _ in range(a.reps):
@@ -53,6 +58,9 @@ print(json.dumps({"path": "decode (tokens -> backbone atom37)", "proteins": a.pr
                   "residues_per_protein": N, "codebook": a.codebook, "df": a.df, "ms_per_batch": round(dt * 1e3, 2),
                   "residues_per_s": round(a.proteins * N / dt, 1), "finite": bool(all(np.isfinite(o).all() for o in out)),
                   "stage_ms": {k: round(v, 3) for k, v in st.items()},
+                  "fold": {"iterations": FOLD_ITERATIONS, "launches_per_iteration": FOLD_LAUNCHES_PER_ITERATION,
+                           "us_per_launch": round(st["fold"] * 1e3 / (FOLD_ITERATIONS * FOLD_LAUNCHES_PER_ITERATION), 1)}
+                  if "fold" in st else None,
                   "roofline": {"kernel": "k_pair_fused (pair chain of the sequence decoder + structure-module pair inputs)",
                                "bound": "mfma", "achieved": round(ex, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(ex / PEAK_FP32_TFLOPS, 4), "mfma_per_32_pair_tile": MFMA_PER_PAIR_TILE,
