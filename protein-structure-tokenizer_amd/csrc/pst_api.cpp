@@ -46,11 +46,13 @@ constexpr double FUSED_HALF_ROUND = 1.02;
 // Fused layers of more than one round run as a persistent queue of half tasks (k_mpnn_q): the
 // unit is 25 edge blocks, so a layer's last units are half as long and its tail half as deep.
 constexpr bool MPNN_QUEUE_DEFAULT = true;
-// Layers that run as the queue (bit l = layer l) when the queue is on: layer 0 (no edge MLP, its
-// edge inputs from the PE tables) runs faster as k_mpnn<0, false> at every size measured —
-// 1 024 / 512 / 256 proteins 8.24-8.30 / 4.15-4.21 / 2.08-2.09 ms against 8.42 / 4.34-4.37 /
-// 2.12 ms as the queue (profiles/r04_ab_qgroup.txt) — layers 1 and 2 gain from it.
-constexpr int64_t MPNN_QUEUE_LAYERS = 6;
+// Layers that run as the queue (bit l = layer l) when the queue is on. Round 4 kept layer 0 as
+// k_mpnn<0, false> (1 024 / 512 / 256 proteins 8.24-8.30 / 4.15-4.21 / 2.08-2.09 ms against 8.42 /
+// 4.34-4.37 / 2.12 ms as the queue, profiles/r04_ab_qgroup.txt); with the wave priorities of round 5
+// in both forms the queue wins for layer 0 too: host to host 1 024 proteins 51.99 vs 52.19 ms, 512
+// 26.79 vs 26.89, 256 13.96 vs 13.99 (8 interleaved rounds, identical tokens;
+// profiles/r06_ab_layer0_queue.txt).
+constexpr int64_t MPNN_QUEUE_LAYERS = 7;
 bool use_half_tasks(int64_t n_tasks, int64_t n_simds) { return 2 * n_tasks > n_simds && n_tasks <= n_simds; }
 bool use_split_schedule(int64_t n_tasks, int64_t n_simds) {
   const int64_t k = (n_tasks + n_simds - 1) / n_simds;

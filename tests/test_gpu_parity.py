@@ -363,12 +363,12 @@ def test_mpnn_queue_identical_at_full_rounds(monkeypatch):
     outs = []
     monkeypatch.setenv("PST_DEBUG", "1")
     monkeypatch.setenv("PST_H2D_CHUNKS", "1")
-    # queue on every layer with the default unit order (groups of one XCD's wave slots), with
-    # adjacent halves (group 0), and the default layers with a group size that leaves a partial
-    # group in every XCD's range (3 072 / 8 = 384 tasks = 10 x 37 + 14)
-    # and the 4-wave queue workgroups
+    # queue on every layer (the default since round 6) with the default unit order (groups of one
+    # XCD's wave slots), with adjacent halves (group 0), layers 1-2 only (the round-4 default, layer 0
+    # one wave per task) with a group size that leaves a partial group in every XCD's range
+    # (3 072 / 8 = 384 tasks = 10 x 37 + 14), and the 4-wave queue workgroups
     for queue, layers, group, qw in (("0", "-", "-", "-"), ("1", "7", "-", "-"), ("1", "7", "0", "-"),
-                                     ("1", "-", "37", "-"), ("1", "-", "-", "4")):
+                                     ("1", "6", "37", "-"), ("1", "-", "-", "4")):
         monkeypatch.setenv("PST_MPNN_QUEUE", queue)
         for k, v in (("PST_MPNN_QUEUE_LAYERS", layers), ("PST_MPNN_QGROUP", group), ("PST_MPNN_QWAVES", qw)):
             if v == "-":
