@@ -200,8 +200,9 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
     """Token ids of this rank's proteins vs the reference's own forward (Vq3D.encode_and_quantize
     under the shim, float64 with JAX's float32 PE argument, i.e. the reference's PE values):
     tests/golden/forward_ref_bench.npz holds EVERY protein of the headline workload (bench256:
-    1 024 proteins, 262 144 tokens) and every 16th of config 5's (bench512), with per-token margins
-    and the bounded latents of the close tokens (refwide.BenchSample). Every mismatch is listed with
+    1 024 proteins, 262 144 tokens) and of config 5's (bench512: 512 proteins, 65 536 tokens), with
+    per-token margins, the bounded latents of the close tokens and every latent of a 32-protein
+    subset of each workload (refwide.BenchSample). Every mismatch is listed with
     its protein, token, latent dim, the reference's margin and our deviation; with `bounded` (our
     FSQ-bounded latents, pst_aux) the report carries our deviation on every close token."""
     try:
@@ -234,6 +235,7 @@ def reference_exact_match(args, ids, tok, off, plan=None, bounded=None):
             "min_margin": r["min_margin"], "close_tokens": r["close_tokens"], "close_below": r["close_below"],
             "max_deviation_close": r["max_deviation_close"],
             "max_deviation_over_margin_close": r["max_deviation_over_margin_close"],
+            "full_latent_proteins": r["full_latent_proteins"], "max_deviation_full": r["max_deviation_full"],
             "mismatches": r["mismatches"], "mismatches_explained_by_rounding": r["mismatches_explained_by_rounding"],
             "unlisted_mismatches": len(r["unlisted"]), "known_cases_not_flipped": r["missing_known"],
             "margin_histogram_all": r["margin_histogram_all"],

@@ -22,7 +22,12 @@ the committed fixture are skipped. The inputs themselves are not stored: they ar
 from `pst_amd.synthetic.synthetic_protein(n_res, 1000 + p)` and must hash to the stored SHA
 (`tests/test_fixture_recipes.py`).
 
-    python tests/golden/make_forward_bench.py --out RAW.npz [--jobs 6] [--stride 1] [--config 3|5]
+Round 6: `--config 5 --stride 1` ran the other 480 proteins of config 5 (all 512 pinned), and
+`--full-subset` re-runs the proteins whose every latent the compact fixture keeps
+(compact_bench.FULL_EVERY / FULL_PHASE: p % 32 == 0 of the headline workload) so the drift of
+tokens that cannot flip is bounded too.
+
+    python tests/golden/make_forward_bench.py --out RAW.npz [--jobs 6] [--stride 1] [--config 3|5] [--full-subset]
     python tests/golden/compact_bench.py RAW.npz [RAW2.npz …]
 """
 import argparse
@@ -78,6 +83,8 @@ def main():
     ap.add_argument("--jobs", type=int, default=7)
     ap.add_argument("--stride", type=int, default=None)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--full-subset", action="store_true",
+                    help="run only the proteins whose every latent compact_bench.py keeps, even if pinned already")
     ap.add_argument("--out", required=True, help="raw per-protein output (merged into the fixture by compact_bench.py)")
     args = ap.parse_args()
     set_config(args.config)
@@ -93,7 +100,13 @@ def main():
     have = set()
     if os.path.exists(OUT) and f"{name}/proteins" in np.load(OUT).files:
         have = {int(p) for p in refwide.load_bench_sample(name).proteins}
-    todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old and p not in have]
+    if args.full_subset:
+        import compact_bench as CB
+        wl = case_name(0).split("_p")[0]
+        todo = [p for p in range(N_PROT) if p % CB.FULL_EVERY[wl] == CB.FULL_PHASE[wl]
+                and f"{case_name(p)}/tokens_pe32" not in old]
+    else:
+        todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old and p not in have]
     print(f"{len(todo)} proteins to run", flush=True)
     done = 0
     with get_context("spawn").Pool(args.jobs) as pool:

@@ -36,7 +36,9 @@ KNOWN_BOUNDARY_CASES = {("bench256", 924, 3): 5}
 # closest token (margin 8.8e-8), which the GPU path resolves as the reference does.
 KNOWN_CPU_BASELINE_CASES = {("bench256", 352, 221): 2}
 # The same list for the CASP14 downsampling fixture: (case, token) -> dim. Measured on all 124 cases
-# (oracle = GPU bits); an unlisted flip, or a listed one that no longer flips, fails.
+# (8 390 tokens; oracle = GPU bits): none flips, the closest reference margin is 5.4e-6 against our
+# deviation of at most 8.1e-6 on other tokens. An unlisted flip, or a listed one that no longer
+# flips, fails.
 KNOWN_CASP_DF_CASES = {}
 # log10 bins of the margin histogram: [0, 1e-7), [1e-7, 1e-6), ..., [1e-1, 0.5]
 EDGES = [0.0, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2, 1e-1, 0.5000001]
@@ -158,6 +160,12 @@ class BenchSample:
         n_res, seed0, cb, df, D, pseed = (int(v) for v in g("meta"))
         self.meta = {"n_res": n_res, "seed0": seed0, "codebook": cb, "df": df, "D": D, "param_seed": pseed}
         self.index = {int(p): i for i, p in enumerate(self.proteins)}
+        # every latent of a fixed protein subset (compact_bench.FULL_EVERY / FULL_PHASE; float32)
+        self.full = {}
+        if f"{name}/full_proteins" in F.files:
+            fo, fb = g("full_tok_off"), g("full_bounded")
+            self.full = {int(p): fb[int(fo[j]):int(fo[j + 1])].astype(np.float64)
+                         for j, p in enumerate(g("full_proteins"))}
 
     def __len__(self):
         return len(self.proteins)
@@ -182,7 +190,7 @@ class BenchSample:
         close_pos = {int(f): j for j, f in enumerate(self.close)}
         n_tok = n_eq = n_close = 0
         mism, unexplained, unlisted = [], [], []
-        dev_close, ratio_close = [], []
+        dev_close, ratio_close, dev_full = [], [], []
         mm_all, mm_bad = [], []
         for k, p in enumerate(prots):
             i = self.index[int(p)]
@@ -197,6 +205,9 @@ class BenchSample:
             mm_all.append(self.margin[a:b])
             mm_bad.append(self.margin[a + bad])
             bo = None if bounded is None else np.asarray(bounded[k], np.float64)[:b - a]
+            if bo is not None and int(p) in self.full:  # every token of a full-latent protein
+                fr = self.full[int(p)]
+                dev_full.append(float(np.abs(bo[:, :fr.shape[1]] - fr).max()))
             # close tokens of this protein: our deviation against the reference's margin per dim
             cl = [(int(f), close_pos[int(f)]) for f in self.close[(self.close >= a) & (self.close < b)]]
             n_close += len(cl)
@@ -235,6 +246,8 @@ class BenchSample:
                 "close_tokens": n_close, "close_below": CLOSE,
                 "max_deviation_close": max(dev_close) if dev_close else None,
                 "max_deviation_over_margin_close": max(ratio_close) if ratio_close else None,
+                "full_latent_proteins": len(dev_full),
+                "max_deviation_full": max(dev_full) if dev_full else None,
                 "margin_histogram_all": histogram(mall), "margin_histogram_mismatches": histogram(mbad),
                 "mismatches": mism + unexplained, "unexplained": unexplained, "unlisted": unlisted,
                 "missing_known": missing,

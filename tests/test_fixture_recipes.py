@@ -43,14 +43,20 @@ def test_casp14_inputs_match_atom37_fixture():
 
 def test_bench_fixture_inputs_reproduce():
     """forward_ref_bench.npz stores no inputs: every protein of bench.py's headline workload (and
-    every 16th of config 5's) must regenerate to the SHA-256 the reference forward ran on."""
-    for name, n_res, want in (("bench256", 256, None), ("bench512", 512, list(range(0, 512, 16)))):
+    of config 5's) must regenerate to the SHA-256 the reference forward ran on. The full-latent
+    subset (compact_bench.FULL_EVERY / FULL_PHASE) agrees with the token ids and margins."""
+    import compact_bench as CB
+    for name, n_res, n_prot in (("bench256", 256, 1024), ("bench512", 512, 512)):
         S = refwide.load_bench_sample(name)
         prots = [int(p) for p in S.proteins]
-        if want is not None:
-            assert prots == want
-        else:
-            assert prots == list(range(1024))
+        assert prots == list(range(n_prot))
+        assert sorted(S.full) == [p for p in prots if p % CB.FULL_EVERY[name] == CB.FULL_PHASE[name]]
+        for p, fb in S.full.items():
+            i = S.index[p]
+            m = S.margin[S.tok_off[i]:S.tok_off[i + 1]]
+            assert fb.shape == (S.n_tokens(p), S.meta["D"])
+            # float32-stored latents: their margins within float32 rounding of the stored ones
+            assert np.abs(refwide.dim_margins(fb).min(-1) - m).max() < 1e-6, (name, p)
         assert S.meta["n_res"] == n_res and S.meta["seed0"] == 1000
         assert len(S.tok_off) == len(prots) + 1 and S.tok_off[-1] == len(S.tokens) == len(S.margin)
         assert (S.margin[S.close] < refwide.CLOSE).all() and (np.delete(S.margin, S.close) >= refwide.CLOSE).all()
