@@ -717,6 +717,12 @@ def main():
             "cpu_baseline_ragged_port": port,
             "casp14_end_to_end": e2e,
         }
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            from provenance import provenance
+            out["provenance"] = provenance()
+        except Exception as ex:  # measurement metadata only
+            out["provenance"] = {"error": str(ex)}
         print(json.dumps(out), flush=True)
     tk.close()
     if world > 1:

@@ -19,6 +19,9 @@ from pst_amd import params as P  # noqa: E402
 from pst_amd._native import Tokenizer  # noqa: E402
 from pst_amd.config import LEVELS  # noqa: E402
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import provenance  # noqa: E402
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--codebook", type=int, default=64000)
 ap.add_argument("--df", type=int, default=1)
@@ -68,5 +71,5 @@ gbs = alg / (ms * 1e-3) / 1e9
 print(json.dumps({"kernel": "k_fsq_aux (+k_row_start, hist memset)", "workload": f"CASP14 31 structures, {T} tokens, K={K}, df={args.df}",
                   "ms_per_launch": round(ms, 4), "bytes_per_launch": alg, "achieved_GBps": round(gbs, 1),
                   "peak_GBps": 8000.0, "frac": round(gbs / 8000.0, 4), "bound": "hbm (write)",
-                  "rows_per_s": round(T / (ms * 1e-3), 1)}))
+                  "rows_per_s": round(T / (ms * 1e-3), 1), "provenance": provenance()}))
 tk.close()

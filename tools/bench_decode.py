@@ -19,6 +19,9 @@ from pst_amd import params as P  # noqa: E402
 from pst_amd._native import Decoder  # noqa: E402
 from pst_amd.config import LEVELS  # noqa: E402
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import provenance  # noqa: E402
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--proteins", type=int, default=8)
 ap.add_argument("--tokens", type=int, default=256)
@@ -65,5 +68,6 @@ print(json.dumps({"path": "decode (tokens -> backbone atom37)", "proteins": a.pr
                                "bound": "mfma", "achieved": round(ex, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(ex / PEAK_FP32_TFLOPS, 4), "mfma_per_32_pair_tile": MFMA_PER_PAIR_TILE,
                                "launch_ms": round(st["k_pair_fused"], 3),
-                               "note": "executed f32 MFMA FLOPs / HIP-event launch time (timed pass without graph replay)"}}))
+                               "note": "executed f32 MFMA FLOPs / HIP-event launch time (timed pass without graph replay)"},
+                  "provenance": provenance()}))
 dec.close()
