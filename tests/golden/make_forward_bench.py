@@ -85,6 +85,8 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--full-subset", action="store_true",
                     help="run only the proteins whose every latent compact_bench.py keeps, even if pinned already")
+    ap.add_argument("--from-protein", type=int, default=0,
+                    help="only proteins >= this (a second generator process working on the top of the range)")
     ap.add_argument("--out", required=True, help="raw per-protein output (merged into the fixture by compact_bench.py)")
     args = ap.parse_args()
     set_config(args.config)
@@ -106,7 +108,8 @@ def main():
         todo = [p for p in range(N_PROT) if p % CB.FULL_EVERY[wl] == CB.FULL_PHASE[wl]
                 and f"{case_name(p)}/tokens_pe32" not in old]
     else:
-        todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old and p not in have]
+        todo = [p for p in proteins(stride) if f"{case_name(p)}/tokens_pe32" not in old and p not in have
+                and p >= args.from_protein]
     print(f"{len(todo)} proteins to run", flush=True)
     done = 0
     with get_context("spawn").Pool(args.jobs) as pool:

@@ -143,14 +143,14 @@ def test_oracle_tokens_equal_reference_bench_sample():
     # longer flips fails
     assert not r["unexplained"] and not r["unlisted"] and not r["missing_known"], r
     assert r["max_deviation_close"] < TOL["_pe32"][1]
-    # the full-latent subset (p % 32 == 0: 8 of these 256) bounds the drift of every token
-    assert r["full_latent_proteins"] == 8 and r["max_deviation_full"] < TOL["_pe32"][1], r
+    # the full-latent subset (p % 32 == 0: all 32 are among these 256) bounds the drift of every token
+    assert r["full_latent_proteins"] == 32 and r["max_deviation_full"] < TOL["_pe32"][1], r
 
 
 def test_oracle_tokens_equal_reference_config5_sample():
     """SURVEY config 5 (codebook 64 000, df 4, 512-residue proteins; all 512 proteins of bench.py's
     --codebook 64000 --df 4 --residues 512 --proteins 512 workload are pinned, the GPU test runs them
-    all): the C oracle on every 4th protein (128 proteins, 16 384 tokens; 16 of them full-latent)
+    all): the C oracle on every 4th protein (128 proteins, 16 384 tokens; the 32 full-latent ones among them)
     against the reference's forward."""
     S = refwide.load_bench_sample("bench512")
     assert S.meta == {"n_res": 512, "seed0": 1000, "codebook": 64000, "df": 4, "D": 6, "param_seed": 1234}
@@ -160,7 +160,7 @@ def test_oracle_tokens_equal_reference_config5_sample():
                              "max_deviation_full", "mismatches")})
     assert r["tokens"] == 16384
     assert not r["unexplained"] and not r["unlisted"] and not r["missing_known"], r
-    assert r["full_latent_proteins"] == 16 and r["max_deviation_full"] < TOL["_pe32"][1], r
+    assert r["full_latent_proteins"] == 32 and r["max_deviation_full"] < TOL["_pe32"][1], r
 
 
 # ------------------------------------------------------------ CASP14 at df 2 / df 4
