@@ -1,7 +1,10 @@
 """Randomised GPU parity sweep: ragged batches of random sizes with randomly missing atoms and
 backbone (filtered residues, short-protein branch), over every codebook / downsampling pair the
 reference ships, against the CPU oracle — token ids exact, bounded codes and pre-projection
-embeddings bitwise. Seeded, so a failure reproduces."""
+embeddings bitwise. Seeded, so a failure reproduces. PST_FUZZ_SEEDS widens the sweep (default 16;
+round 6 ran 256 once, profiles/r06_gpu_fuzz_256.txt)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -31,7 +34,7 @@ def _damaged(n, seed, rng):
     return s._replace(atom37_gt_exists=gt)
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("PST_FUZZ_SEEDS", "16"))))
 def test_random_batches_match_oracle(seed):
     from pst_amd._native import pack_samples
     rng = np.random.default_rng(1000 + seed)
