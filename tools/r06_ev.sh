@@ -1,6 +1,6 @@
 # Round 6 evidence on the final build: GPU suite + smoke, the default bench line, full-size kernel trace (one
 # chunk) and the default bench's kernel trace, PMC passes (traffic + issue counters), config-4 aux, decode bench
-# (three shapes), strong-scaling shares, CASP14 kernel trace. PST_HEAD (the commit) comes from the command line.
+# (three shapes), strong-scaling shares, CASP14 kernel trace, the config-5 bench line. PST_HEAD (the commit) comes from the command line.
 # usage: PST_HEAD=<commit> bash tools/r06_ev.sh TAG [PYTEST_K]
 set -e
 TAG=${1:-r06ev}
@@ -32,4 +32,6 @@ echo decode ok
 timeout -k 10 900 bash tools/strong_scaling_shares.sh > gpurun_out/${TAG}_shares.jsonl 2>&1
 echo shares ok
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_casp -o run -- python tools/prof_casp14.py --reps 20 > gpurun_out/${TAG}_casp.log 2>&1
+echo casp ok
+timeout -k 10 400 python -u bench.py --codebook 64000 --df 4 --residues 512 --proteins 512 --no-e2e --cpu-sample 32 > gpurun_out/${TAG}_bench_cfg5.json 2> gpurun_out/${TAG}_bench_cfg5.err
 echo done
