@@ -224,6 +224,7 @@ struct pst_ctx {
   size_t down_w = 0, down_b = 0;
   // tables (device, separate allocations)
   float *d_h0 = nullptr, *d_PM0 = nullptr, *d_T = nullptr, *d_U = nullptr, *d_RPE = nullptr;
+  float* d_V0 = nullptr;  // [512][512][128]: layer 0's per-(receiver, sender) message chain start
   float fsq_half[8]{}, fsq_off[8]{}, fsq_shift[8]{};
   int fsq_L[8]{}, fsq_basis[8]{};
   // workspace (grow-only)
@@ -476,6 +477,7 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   HIPCHK(hipMalloc(&ctx->d_PM0, 512 * 256 * sizeof(float)));
   HIPCHK(hipMalloc(&ctx->d_T, 1023 * 128 * sizeof(float)));
   HIPCHK(hipMalloc(&ctx->d_U, 1023 * 128 * sizeof(float)));
+  HIPCHK(hipMalloc(&ctx->d_V0, (size_t)512 * 512 * 128 * sizeof(float)));
   HIPCHK(hipMalloc(&ctx->d_RPE, (size_t)ctx->max_out * 128 * sizeof(float)));
   HIPCHK(hipMemcpy(ctx->d_RPE, rpe.data(), rpe.size() * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&ctx->d_clk, 24 * sizeof(unsigned long long)));
@@ -490,6 +492,8 @@ int build_weights(pst_ctx* ctx, const float* blob) {
   pst::launch_table_gemm(a + o_epe, 1023, F4(o_ee_w), nullptr, a + ctx->emb_b, ctx->d_T, 128, ctx->stream);
   // U = T · msg0 W[256:384]: the edge-PE half of layer 0's message first layer
   pst::launch_table_gemm(ctx->d_T, 1023, F4(ctx->L[0].msg.w0), nullptr, nullptr, ctx->d_U, 128, ctx->stream);
+  // V0 = (PM0_s[ls] + PM0_r[lr]) + U[ls - lr] per (lr, ls): 128 MB, one row per layer-0 edge
+  pst::launch_pair_table(ctx->d_PM0, ctx->d_U, ctx->d_V0, ctx->stream);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(ctx->stream));
   // FSQ constants (quantize.py:175-181, computed in float32 as JAX does)
@@ -748,6 +752,7 @@ int run(pst_ctx* ctx, const double* d_pos, const uint8_t* d_flags, const int64_t
     m.b_embed = A + ctx->emb_b;
     m.PM0 = ctx->d_PM0;
     m.Utab = ctx->d_U;
+    m.V0 = ctx->d_V0;
     m.W_msg0f = F4(ctx->w_msg0f);
     m.h0tab = ctx->d_h0;
     if (l > 0) {
@@ -967,7 +972,7 @@ int pst_destroy(pst_ctx* ctx) {
     if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
   if (ctx->aux) (void)hipFree(ctx->aux);
   if (ctx->msg) (void)hipFree(ctx->msg);
-  for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_U, (void*)ctx->d_RPE, ctx->ws})
+  for (void* p : {(void*)ctx->d_arena, (void*)ctx->d_h0, (void*)ctx->d_PM0, (void*)ctx->d_T, (void*)ctx->d_U, (void*)ctx->d_V0, (void*)ctx->d_RPE, ctx->ws})
     if (p) (void)hipFree(p);
   if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
   if (ctx->h_tokens) (void)hipHostFree(ctx->h_tokens);

@@ -71,6 +71,7 @@ struct MpnnArgs {
   const float* b_embed;    // perm (folded into Ttab: unused by the kernel)
   const float* PM0;        // [512][256] perm: h0 · msg0 W[0:128] | W[128:256]
   const float* Utab;       // [1023][128] perm: T · msg0 W[256:384] (layer-0 message)
+  const float* V0;         // [512][512][128] perm: (PM0_s[ls] + PM0_r[lr]) + Utab[ls - lr] (k_pair_table)
   const float4* W_msg0f;   // [16][64] float4: init_edge_embed rows 128..154 · msg0 W[256:384]
   const float* h0tab;      // [512][128] perm: init_node_embed(node PE)
   // layers >= 1
@@ -223,6 +224,7 @@ enum { DOWN_ONE_WAVE = 0, DOWN_COOP = 1, DOWN_PAIR = 2 };
 void launch_down(int df, const DownArgs& a, int form, hipStream_t st);
 void launch_fsq_aux(const FsqAuxArgs& a, int n_prot, hipStream_t st);
 // Y = (init or 0) + X·W (+ b): init / b perm-ordered 128-vectors (either may be null)
+void launch_pair_table(const float* PM0, const float* U, float* V, hipStream_t st);
 void launch_table_gemm(const float* X, int n_rows, const float4* Wf, const float* b, const float* init, float* Y,
                        int ldy, hipStream_t st);
 

@@ -551,6 +551,9 @@ __device__ __forceinline__ int32_t edge_sender(const MpnnArgs& a, int64_t g0, in
   return a.senders[g0 * KNN + 32 * blk + (lane & 31)];
 }
 
+#ifndef L0_PAIR_TABLE
+#define L0_PAIR_TABLE 1
+#endif
 #ifndef E_STORE_SPREAD
 #define E_STORE_SPREAD 1
 #endif
@@ -601,8 +604,12 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
     // first layer through the embedding's factors: e0·W = T[s-r]·W + f·(Wf·W),
     // so the chain starts from (h_s·W_s + (b + h_r·W_r)) + U[s-r] and runs over the 32
     // features: 16 k-steps instead of 64
-    tile_add_rows(m, a.PM0 + (int64_t)ls0 * 256 + 0, a.PM0 + (int64_t)lr0 * 256 + 128);
-    tile_add_row(m, a.Utab + (int64_t)(ls0 - lr0 + 511) * 128);
+    if (L0_PAIR_TABLE) {  // the same sums, precomputed per (lr, ls): one gathered row, no adds
+      tile_load_perm(m, a.V0 + ((int64_t)lr0 * 512 + ls0) * 128);
+    } else {
+      tile_add_rows(m, a.PM0 + (int64_t)ls0 * 256 + 0, a.PM0 + (int64_t)lr0 * 256 + 128);
+      tile_add_row(m, a.Utab + (int64_t)(ls0 - lr0 + 511) * 128);
+    }
     if (E_STORE_SPREAD)  // e leaves during this GEMM, after the gathers above (tile_gemm_store)
       feat_gemm_st<true>(m, x, a.W_msg0f, &e, make_rsrc_or_null(a.e_out ? a.e_out + eblk : nullptr));
     else
@@ -1854,7 +1861,29 @@ __global__ __launch_bounds__(256) void k_table_gemm(const float* __restrict__ X,
   if (row < n_rows) tile_store_perm(acc, Y + (int64_t)row * ldy);
 }
 
+// V0[lr][ls] = (PM0_s[ls] + PM0_r[lr]) + U[ls - lr] for lr, ls < 512 (perm rows): layer 0's message
+// chain start as one gathered row per edge, the same two additions in the same order as edge_block
+// does them from the three tables (L0_PAIR_TABLE).
+__global__ __launch_bounds__(256) void k_pair_table(const float4* __restrict__ PM0, const float4* __restrict__ U,
+                                                    float4* __restrict__ V) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 of V
+  const int c = (int)(i & 31), ls = (int)((i >> 5) & 511), lr = (int)(i >> 14);
+  const float4 a = PM0[ls * 64 + c], b = PM0[lr * 64 + 32 + c], u = U[(ls - lr + 511) * 32 + c];
+  float4 v;
+  v.x = (a.x + b.x) + u.x;
+  v.y = (a.y + b.y) + u.y;
+  v.z = (a.z + b.z) + u.z;
+  v.w = (a.w + b.w) + u.w;
+  V[i] = v;
+}
+
 // --------------------------------------------------------------------------- launchers
+void launch_pair_table(const float* PM0, const float* U, float* V, hipStream_t st) {
+  hipLaunchKernelGGL(k_pair_table, dim3(512 * 512 * 32 / 256), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(PM0), reinterpret_cast<const float4*>(U),
+                     reinterpret_cast<float4*>(V));
+}
+
 void launch_prep(const PrepArgs& a, int n_prot, hipStream_t st) {
   if (n_prot <= 0) return;
   if (a.pos32) hipLaunchKernelGGL(k_prep<true>, dim3(n_prot), dim3(512), 0, st, a);
