@@ -111,6 +111,11 @@ void env_threshold(int64_t& v, const char* name) {
 thread_local std::string g_create_error;
 
 
+// float index of slot `slot` of edge e in the blocked feature layout (pst::feat_f4), and the floats
+// that n_edges edges occupy (whole 32-edge blocks)
+inline size_t feat_float(size_t e, int slot) { return (size_t)pst::feat_f4((int64_t)e, slot >> 2) * 4 + (slot & 3); }
+inline size_t feat_floats(size_t n_edges) { return (n_edges + 31) / 32 * 32 * 32; }
+
 // ------------------------------------------------------------------ parameter views
 struct Lin {
   const float* w;
@@ -1530,7 +1535,7 @@ int pst_build_graph(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_fl
   rc = run(ctx, w.pos, w.flags, offsets, n_prot, w.tokens, w.n_tok, w.n_nodes, /*graph_only=*/true);
   if (rc) return rc;
   std::vector<int32_t> snd((size_t)R * KNN);
-  std::vector<float> feat((size_t)R * KNN * 32);
+  std::vector<float> feat(feat_floats((size_t)R * KNN));
   HIPCHK(hipMemcpyAsync(snd.data(), w.senders, sizeof(int32_t) * snd.size(), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipMemcpyAsync(feat.data(), w.feat, sizeof(float) * feat.size(), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipMemcpyAsync(ca_out, w.ca, sizeof(double) * 3 * R, hipMemcpyDeviceToHost, ctx->stream));
@@ -1544,7 +1549,7 @@ int pst_build_graph(pst_ctx* ctx, const double* atom_pos, const uint8_t* atom_fl
       for (int j = 0; j < KNN; ++j) {
         const size_t e = (size_t)g * KNN + j;
         senders_out[e] = real && snd[e] >= 0 ? (int32_t)(snd[e] - base) : -1;
-        for (int c = 0; c < 27; ++c) edge_features_out[e * 27 + c] = real ? feat[e * 32 + pst::feat_slot(c)] : 0.0f;
+        for (int c = 0; c < 27; ++c) edge_features_out[e * 27 + c] = real ? feat[feat_float(e, pst::feat_slot(c))] : 0.0f;
       }
       if (!real) ca_out[3 * g] = ca_out[3 * g + 1] = ca_out[3 * g + 2] = 0.0;
     }
@@ -1722,11 +1727,11 @@ int pst_debug_fetch(pst_ctx* ctx, int32_t which, void* out, size_t bytes) {
   if (which == 10) {  // 32-float rows in feature order (features 0..26, then +0), from feat_slot's
     need = (size_t)ctx->last_R * KNN * 32 * sizeof(float);
     if (bytes < need) return fail(ctx, PST_E_INVALID, "debug buffer too small");
-    tmp.resize(need / sizeof(float));
-    HIPCHK(hipMemcpy(tmp.data(), ctx->w.feat, need, hipMemcpyDeviceToHost));
+    tmp.resize(feat_floats((size_t)ctx->last_R * KNN));
+    HIPCHK(hipMemcpy(tmp.data(), ctx->w.feat, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
     float* o = (float*)out;
     for (size_t e = 0; e < (size_t)ctx->last_R * KNN; ++e)
-      for (int f = 0; f < 32; ++f) o[e * 32 + f] = f < pst::FEAT_USED ? tmp[e * 32 + pst::feat_slot(f)] : 0.0f;
+      for (int f = 0; f < 32; ++f) o[e * 32 + f] = f < pst::FEAT_USED ? tmp[feat_float(e, pst::feat_slot(f))] : 0.0f;
     return PST_OK;
   } else if (which == 13 || which == 14) {  // the last call's input rows: positions f32 (pst_tokenize_f32 /
     // pst_tokenize_pdb_batch / pst_tokenize_pdb_files) [R,37,3], flags [R,37]

@@ -18,6 +18,12 @@ __host__ __device__ constexpr int slot_feat(int s) {
   return s < 25 ? s : s == 25 ? 26 : s == 28 ? 25 : -1;
 }
 constexpr int FEAT_USED = 27;
+// Edge features in HBM, blocked by 32 edges (edge E = receiver slot · 50 + neighbour; a task's
+// 50 blocks are consecutive): float4 q of edge E (slots 4q .. 4q+3) sits at float4 index
+// feat_f4(E, q) — per block 4 KB as [q >> 1][q & 1][E & 31] — so layer 0's lane (half h, edge e),
+// which needs float4s 2i + h (i = 0..3), reads each i as one lane-linear 1 KB load
+__host__ __device__ constexpr int feat_f4_q(int q) { return (q >> 1) * 64 + (q & 1) * 32; }
+__host__ __device__ constexpr int64_t feat_f4(int64_t E, int q) { return (E >> 5) * 256 + (E & 31) + feat_f4_q(q); }
 
 struct PrepArgs {
   const double* pos;       // [R,37,3]

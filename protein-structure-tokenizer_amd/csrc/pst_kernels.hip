@@ -152,7 +152,7 @@ __device__ __forceinline__ double dot3(const double* b, const double* x) {
 }
 
 __device__ void edge_features(const double* fr_r, const double* fr_s, const double* ca_r,
-                              const double* ca_s, double dist, float* __restrict__ out) {
+                              const double* ca_s, double dist, float4* __restrict__ o) {
   float f[FEAT_USED];
   double d2 = dist * dist;
   double ls = 1.0;
@@ -173,9 +173,8 @@ __device__ void edge_features(const double* fr_r, const double* fr_s, const doub
   // stored in the feature GEMMs' slot order (feat_slot), padding slots +0 (picked per slot at
   // compile time: a second 32-float array here cost k_knn 24 VGPRs and three waves per SIMD)
   auto v = [&](int sl) { return slot_feat(sl) < 0 ? 0.0f : f[slot_feat(sl)]; };
-  float4* o = reinterpret_cast<float4*>(out);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) o[q] = make_float4(v(4 * q), v(4 * q + 1), v(4 * q + 2), v(4 * q + 3));
+  for (int q = 0; q < 8; ++q) o[feat_f4_q(q)] = make_float4(v(4 * q), v(4 * q + 1), v(4 * q + 2), v(4 * q + 3));
 }
 
 __device__ __forceinline__ bool lex_less(double d1, int s1, double d2, int s2) {
@@ -220,12 +219,13 @@ __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
   if (g >= a.n_slots) return;
   const int loc = a.node_local[g];
   int32_t* snd = a.senders + g * KNN;
-  float* feat = a.feat + g * KNN * 32;
+  // this lane's edge E = g * KNN + lane in the blocked layout: float4 q at o[feat_f4_q(q)]
+  const int64_t E = g * KNN + lane;
+  float4* o = reinterpret_cast<float4*>(a.feat) + feat_f4(E, 0);
   if (loc < 0) {  // gap / padding slot: self edges, zero features, degree 0
     if (lane < KNN) {
       snd[lane] = (int32_t)g;
-      float4* o = reinterpret_cast<float4*>(feat + lane * 32);
-      for (int q = 0; q < 8; ++q) o[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = 0; q < 8; ++q) o[feat_f4_q(q)] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (lane == 0) a.deg[g] = 0;
     return;
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
     if (n >= KNN) {
       snd[lane] = (int32_t)(base + my_s);
       edge_features(a.frame + g * 9, a.frame + (base + my_s) * 9, a.ca + g * 3, a.ca + (base + my_s) * 3, my_d,
-                    feat + lane * 32);
+                    o);
     } else {
       // n < k (preprocessing.py:229-260): senders stay per-row, features keep the n*n order
       snd[lane] = lane < n ? (int32_t)(base + my_s) : (int32_t)g;
@@ -364,10 +364,9 @@ __global__ __launch_bounds__(256) void k_knn(KnnArgs a) {
         double ds;
         int s = rank_select(a.cen, base, n, rr, cc, &ds);
         edge_features(a.frame + (base + rr) * 9, a.frame + (base + s) * 9, a.ca + (base + rr) * 3,
-                      a.ca + (base + s) * 3, ds, feat + lane * 32);
+                      a.ca + (base + s) * 3, ds, o);
       } else {
-        float4* o = reinterpret_cast<float4*>(feat + lane * 32);
-        for (int q = 0; q < 8; ++q) o[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = 0; q < 8; ++q) o[feat_f4_q(q)] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   }
@@ -557,13 +556,24 @@ __device__ __forceinline__ int32_t edge_sender(const MpnnArgs& a, int64_t g0, in
 #ifndef E_STORE_SPREAD
 #define E_STORE_SPREAD 1
 #endif
+// Layer 0: this lane's edge features of block `blk` (edges g0·50 + 32·blk + e: a task's edges are
+// consecutive), x[r] = slots (r&3) + 8(r>>2) + 4·half as feat_gemm reads them: float4 2i + half of
+// its edge, which the blocked layout (feat_f4) holds at lane-linear position i·64 + lane
+__device__ __forceinline__ void edge_feat(const MpnnArgs& a, int64_t g0, int lane, int blk, float (&x)[16]) {
+  const float4* fp = reinterpret_cast<const float4*>(a.feat) + ((g0 / 32) * KNN + blk) * 256 + lane;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 v = fp[64 * i];
+    x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+  }
+}
+
 template <int LAYER, int KL = w1_lds_ksteps<LAYER>()>
 __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int64_t g0, int lane, int blk,
                                            int32_t s_pre, Tile& m, const float4* w1_lds = nullptr) {
   const int te = 32 * blk + (lane & 31);
   const int rl = te / 50;
   const int64_t g = g0 + rl;
-  const int64_t E = g * KNN + (te - 50 * rl);
   const int64_t s = s_pre;
   const int64_t eblk = (task * 50 + blk) * 4096;
   Tile e;
@@ -580,12 +590,7 @@ __device__ __forceinline__ void edge_block(const MpnnArgs& a, int64_t task, int6
     lr0 = lr;
     ls0 = lr + d;
     tile_load_perm(e, a.Ttab + (int64_t)(d + 511) * 128);
-    const float4* fp = reinterpret_cast<const float4*>(a.feat + E * 32 + 4 * (lane >> 5));
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float4 v = fp[2 * q];
-      x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
-    }
+    edge_feat(a, g0, lane, blk, x);
     feat_gemm(e, x, a.W_embed);
   } else {
     // edge update of layer LAYER-1: e = LN(e + MLP([h_s | h_r | e]))
