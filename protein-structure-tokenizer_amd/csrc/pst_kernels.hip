@@ -389,11 +389,36 @@ __device__ __forceinline__ float umask(uint32_t bits) {
   return r;
 }
 // the two chains over the 32 edges of a block (v: this lane's channel row, edges in order)
+#ifndef SEG_PACKED
+#define SEG_PACKED 1
+#endif
+#if SEG_PACKED
+// Both chains in ONE packed FMA per edge (round 6): (accA, accB) = (v_e, v_e)·(mA_e, mB_e) +
+// (accA, accB), v_e broadcast from its register pair by op_sel, the mask pair from SGPRs — per
+// half exactly the fmaf of the scalar form, so the same bits at half the VALU issue
+template <int EE>
+__device__ __forceinline__ void seg_step(f32x2& acc, f32x2 vp, uint32_t mA, uint32_t mB) {
+  const f32x2 m = {umask<EE>(mA), umask<EE>(mB)};
+  if (EE & 1)
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(vp), "s"(m));
+  else
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(vp), "s"(m));
+}
+template <int... EE>
+__device__ __forceinline__ void seg_chains(const float (&v)[32], uint32_t mA, uint32_t mB, float& accA, float& accB,
+                                           std::integer_sequence<int, EE...>) {
+  f32x2 acc = {accA, accB};
+  (seg_step<EE>(acc, (f32x2){v[EE & ~1], v[EE | 1]}, mA, mB), ...);
+  accA = acc.x;
+  accB = acc.y;
+}
+#else
 template <int... EE>
 __device__ __forceinline__ void seg_chains(const float (&v)[32], uint32_t mA, uint32_t mB, float& accA, float& accB,
                                            std::integer_sequence<int, EE...>) {
   ((accA = __builtin_fmaf(v[EE], umask<EE>(mA), accA), accB = __builtin_fmaf(v[EE], umask<EE>(mB), accB)), ...);
 }
+#endif
 
 // acc = a_row + b_row (perm rows); b is streamed 4 values at a time so the sum needs one tile
 // of registers, not two
