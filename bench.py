@@ -4,20 +4,24 @@ Workload (SURVEY config 3): 1 024 synthetic proteins × 256 residues = 262 144 r
 df = 1, batch-sharded over the N GPUs of the job (LPT on residues: 128 proteins per GPU at N = 8;
 "scaling": "strong", total work fixed). `--weak` instead gives every GPU its own 1 024 proteins.
 
-One step = BASELINE.md §4's timed region on every rank: atom37 arrays in pinned host memory →
-H2D → graph build → 3 MPNN layers → downsampler → FSQ → D2H token ids (`pst_tokenize_f32`: the
-float32 coordinates the PDB path holds, widened to float64 on the GPU with identical results;
-`--f64-input` times `pst_tokenize` on float64 arrays, and the other format is reported beside it;
-one synchronous call per rank; libpst pipelines the H2D of protein chunks with the compute). W
-warm-up steps, then K timed steps bracketed by barrier + synchronize; each step is also timed
-on its own, the per-step time is the max over ranks, `ms_per_step` is the median of the K and
-`value` = all residues of the job / that median.
+One step = one tokenization of the rank's whole batch with its inputs already resident in HBM
+(the task's `value` contract): atom37 positions (float64) + flags in device memory → graph build
+→ 3 MPNN layers → downsampler → FSQ → token ids in device memory (`pst_tokenize_device`,
+synchronised per step). W warm-up steps, then K timed steps bracketed by barrier + synchronize;
+each step is also timed on its own, the per-step time is the max over ranks, `ms_per_step` is the
+median of the K and `value` = all residues of the job / that median.
+
+Reported beside it, never as `value`: BASELINE.md §4's PCIe-inclusive region (`host_to_host`):
+atom37 in pinned host memory → H2D → … → D2H token ids (`pst_tokenize_f32`, the PDB path's float32
+coordinates; `--f64-input` times `pst_tokenize` on float64 arrays, and the other format is
+reported beside it; libpst pipelines the H2D of protein chunks with the compute), K steps, median,
+max over ranks. Its tokens must equal the device-resident step's (checked).
 
 Launch: `python bench.py` (1 GPU); `python bench.py --gpus N` spawns N worker processes itself
 (the parent never touches the GPU); under `torch.distributed.run` each rank is one GPU (RCCL for
 the barrier and the max-over-ranks reductions; no collective on the data path).
 
-Also reported on rank 0: the device-resident rate (inputs already in HBM), the dominant kernel's
+Also reported on rank 0: the dominant kernel's
 roofline from HIP events on the library's stream (executed MFMA FLOPs / launch time / f32 MFMA
 peak), per-kernel fractions, exact match vs the reference's own forward on the fixture proteins
 of the workload (tests/golden/forward_ref_wide.npz) and vs the C oracle, the CPU baselines
@@ -524,9 +528,24 @@ def main():
     tk = Tokenizer(gpu, args.codebook, args.df, blob)
     torch.cuda.synchronize(dev)
 
+    # inputs resident in HBM before the timed region (the `value` contract): float64 positions and
+    # flags on the device, tokens left in HBM; the host-to-host rate (pinned host atom37 -> H2D ->
+    # tokens -> D2H, PCIe included) is measured after it and reported beside it, never as `value`
+    d_pos = pin_pos.to(dev)
+    d_flags = pin_flags.to(dev)
+    d_tok = torch.zeros(R, dtype=torch.int32, device=dev)
+    d_ntok = torch.zeros(len(samples), dtype=torch.int32, device=dev)
+    d_nn = torch.zeros(len(samples), dtype=torch.int32, device=dev)
+
+    def dstep():
+        tk.tokenize_device(d_pos.data_ptr(), d_flags.data_ptr(), off, d_tok.data_ptr(), d_ntok.data_ptr(),
+                           d_nn.data_ptr())
+
     log(f"rank {rank}: {len(samples)} proteins, {R} residues; warm-up")
     for _ in range(args.warmup):
         tk.tokenize_packed(ppos, pflags, off)
+        dstep()
+        tk.sync()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -539,14 +558,15 @@ def main():
     t_start = time.perf_counter()
     for _ in range(args.steps):
         t0 = time.perf_counter()
-        tok, nt, nn = tk.tokenize_packed(ppos, pflags, off)  # host → host, synchronous
+        dstep()  # HBM-resident inputs -> graph -> encoder -> FSQ -> token ids in HBM
+        tk.sync()
         times.append(time.perf_counter() - t0)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     clock = clock_stats([tk.clock_counters(reset=True)], steps=args.steps)
-    plan = tk.last_plan_detail()  # chunks and layer schedule of the timed step (rank 0's share)
+    tk.set_clock_counters(False)
     log(f"rank {rank}: {args.steps} timed steps in {elapsed:.2f} s")
     stats = torch.tensor(times + [elapsed], dtype=torch.float64, device=red_dev)
     total_res = torch.tensor([R], dtype=torch.float64, device=red_dev)
@@ -559,6 +579,27 @@ def main():
     job_res = int(total_res.item())
     med = float(np.median(step_s))
     value = job_res / med
+    dev_tok = d_tok.cpu().numpy().view(np.uint32)
+
+    # host to host (PCIe included): the same steps from pinned host buffers through pst_tokenize_f32
+    # (or pst_tokenize with --f64-input), median over as many steps, max over ranks
+    h_times = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        tok, nt, nn = tk.tokenize_packed(ppos, pflags, off)  # host -> host, synchronous
+        h_times.append(time.perf_counter() - t0)
+    plan = tk.last_plan_detail()  # chunks and layer schedule of the host-to-host step (rank 0's share)
+    h_stats = torch.tensor([float(np.median(h_times))], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        dist.all_reduce(h_stats, op=dist.ReduceOp.MAX)
+    h_med = float(h_stats.cpu().numpy()[0])
+    host_to_host = {"residues_per_s": round(job_res / h_med, 1), "ms_per_step": round(h_med * 1e3, 3),
+                    "steps": args.steps,
+                    "tokens_identical_to_device_resident": bool(np.array_equal(tok[:R], dev_tok[:R])),
+                    "note": ("pinned host atom37 -> H2D -> graph -> encoder -> FSQ -> D2H token ids ("
+                             + ("pst_tokenize, float64 positions" if args.f64_input else
+                                "pst_tokenize_f32, float32 positions as the PDB path holds them")
+                             + "), median over steps of the max over ranks; PCIe-inclusive, not `value`")}
 
     # the other wire format on the same inputs: same tokens, and its host-to-host time (median of 5)
     alt = ppos64 if not args.f64_input else pin_pos32.numpy()
@@ -572,9 +613,11 @@ def main():
     other_input = {"input": "float64 (pst_tokenize)" if not args.f64_input else "float32 (pst_tokenize_f32)",
                    "residues_per_s_per_gpu": round(R / alt_med, 1), "ms": round(alt_med * 1e3, 3),
                    "tokens_identical": bool(np.array_equal(tok_alt[:R], tok[:R])),
-                   "note": "rank 0's shard, median of 5 after one warm-up"}
+                   "note": "rank 0's shard, host to host, median of 5 after one warm-up"}
 
-    # exact match vs the reference fixtures of the proteins this rank holds (summed over ranks)
+    # exact match vs the reference fixtures of the proteins this rank holds (summed over ranks), on
+    # the host-to-host step's tokens (identical to the timed device-resident ones, checked above)
+    tok, nt, nn = tk.tokenize_packed(ppos, pflags, off)
     ref_match = reference_exact_match(args, ids, tok, off, plan, bounded=tk.aux(R)["bounded"])
     if world > 1:
         cnt = torch.tensor([ref_match["tokens_compared"], ref_match["identical"]] if ref_match else [0, 0],
@@ -584,24 +627,8 @@ def main():
             ref_match["tokens_compared_all_ranks"] = int(cnt[0].item())
             ref_match["identical_all_ranks"] = int(cnt[1].item())
 
-    # device-resident rate + per-stage device times (HIP events on libpst's stream), rank 0's share
-    d_pos = pin_pos.to(dev)
-    d_flags = pin_flags.to(dev)
-    d_tok = torch.zeros(R, dtype=torch.int32, device=dev)
-    d_ntok = torch.zeros(len(samples), dtype=torch.int32, device=dev)
-    d_nn = torch.zeros(len(samples), dtype=torch.int32, device=dev)
-
-    def dstep():
-        tk.tokenize_device(d_pos.data_ptr(), d_flags.data_ptr(), off, d_tok.data_ptr(), d_ntok.data_ptr(),
-                           d_nn.data_ptr())
-    dstep()
-    tk.sync()
-    dts = []
-    for _ in range(5):
-        t0 = time.perf_counter()
-        dstep()
-        tk.sync()
-        dts.append(time.perf_counter() - t0)
+    # per-stage device times (HIP events on libpst's stream), rank 0's share
+    tk.set_clock_counters(True)
     tk.set_timing(True)
     stage = None
     sclk = []
@@ -690,23 +717,20 @@ def main():
                        "proteins_job": args.proteins * (world if args.weak else 1), "residues_job": job_res,
                        "proteins_rank0": len(ids), "parallelism": f"dp{world} (independent proteins, LPT shard)",
                        "world_size_seen": seen_world, "dist_backend": args.dist_backend if world > 1 else None},
-            "timed_region": ("pinned host atom37 -> H2D -> graph -> encoder -> FSQ -> D2H token ids ("
-                             + ("pst_tokenize, float64 positions" if args.f64_input else
-                                "pst_tokenize_f32, float32 positions as the PDB path holds them")
-                             + "), median over steps of the max over ranks"),
+            "timed_region": ("atom37 (float64) + flags already resident in HBM -> graph -> encoder -> FSQ -> token "
+                             "ids in HBM (pst_tokenize_device, synchronised per step), median over steps of the "
+                             "max over ranks"),
+            "host_to_host": host_to_host,
             "other_input_format": other_input,
             "pipeline_plan": plan,
             "ms_per_step_mean_bracketed": round(elapsed / args.steps * 1e3, 3),
             "elapsed_s": round(elapsed, 3),
-            "device_resident": {"residues_per_s_per_gpu": round(R / float(np.median(dts)), 1),
-                                "ms": round(float(np.median(dts)) * 1e3, 3),
-                                "note": "rank 0's shard with inputs already in HBM (pst_tokenize_device), median of 5"},
             "clock": clock,
             "ms_per_step_at_2p4ghz": (round(med * 1e3 * clock["mean_ghz"] / SPEC_GHZ, 3) if clock else None),
             "clock_note": ("shader clock of the timed steps (rank 0): s_memtime / s_memrealtime stamps of the "
                            "fused MPNN launches (pst_clock_counters), per step over its three layers; "
                            "ms_per_step_at_2p4ghz scales the median step by mean_ghz / 2.4 as if all of it "
-                           "were clock-bound (the H2D part is not)"),
+                           "were clock-bound"),
             "roofline": roofline,
             "exact_match_reference": ref_match,
             "exact_match": exact,

@@ -10,8 +10,11 @@ for P in 1024 512 256 128; do
 import json, sys
 P = int(sys.argv[1]); N = 1024 // P
 d = json.load(open(f"gpurun_out/shares_{P}.json"))
+# `ms_per_step` / `value`: inputs resident in HBM (bench.py's timed region since round 6); before, the
+# host-to-host step, now `host_to_host`
+h = d.get("host_to_host") or {}
 print(json.dumps({"n_gpus_simulated": N, "proteins_per_gpu": P, "ms_per_step": d["ms_per_step"],
                   "per_gpu_residues_per_s": d["value"], "job_residues_per_s_if_N_gpus": round(d["value"] * N, 1),
-                  "device_resident_ms": d["device_resident"]["ms"], "stage_ms": d["roofline"]["stage_ms"]}))
+                  "host_to_host_ms": h.get("ms_per_step"), "stage_ms": d["roofline"]["stage_ms"]}))
 PY
 done
